@@ -1,0 +1,167 @@
+#!/usr/bin/env python
+"""Headline benchmark: SD-1.5 512² 50-step images/sec (whole node) + p50 guess-score latency.
+
+BASELINE.json config 3: concurrent rooms data-parallel over the node's GPUs, one process per
+GPU, SD-1.5 512×512, 50 PNDM steps (51 UNet evaluations, SD-1.5's default scheduler),
+classifier-free guidance 7.5 (UNet batch 2×4), batch = 4 images per room, bf16, random-init
+weights, synthetic ``seeds.txt`` story prompts.  One benchmark *step* = every rank generates
+its room's 4 images end to end (CLIP encode → hipGraph-replayed denoise loop → VAE decode →
+uint8) and the images are all-gathered to rank 0 over RCCL (what the front-end does at a
+round boundary).  Whole-job images/s = N·4·K / max-over-ranks(time of K steps).
+
+Rank 0 also measures the streaming guess scorer (BASELINE config 1/5): MiniLM-L6 embed +
+cosine for a 64-player micro-batch, p50 latency in ms (reported as ``p50_score_ms``).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4] [--baseline]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_IMAGES_PER_SEC = None  # BASELINE.json "published": {} — no reference number
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=4, help="images per room (per GPU)")
+    p.add_argument("--model", default="sd15")
+    p.add_argument("--denoise-steps", type=int, default=50)
+    p.add_argument("--scheduler", default="pndm")
+    p.add_argument("--baseline", action="store_true", help="stock PyTorch ops, no graphs (eager baseline)")
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--no-score", action="store_true")
+    p.add_argument("--fp8-attention", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    if args.baseline:
+        os.environ["CASSMANTLE_OPS"] = "torch"
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from cassmantle_amd import ops
+    from cassmantle_amd.parallel import dist as cdist
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
+
+    ctx = cdist.init_from_env()
+    rank, world = ctx.rank, ctx.world_size
+    device = ctx.device
+    if args.baseline:
+        ops.set_mode("torch")
+    torch.manual_seed(0)
+
+    spec = SPECS[args.model]
+    sd = StableDiffusion(spec, device=device, use_graphs=not (args.baseline or args.no_graphs),
+                         fp8_attention=args.fp8_attention, seed=0)
+    gen = SyntheticPromptGenerator(salt=rank)
+    seeds_txt, styles = load_seeds(), load_styles()
+    negative = "blurry, distorted, fake, abstract, negative"
+
+    def room_prompts(step: int):
+        out = []
+        for j in range(args.batch):
+            title = seeds_txt[(rank * 7 + step * 3 + j) % len(seeds_txt)]
+            text = gen.generate(title + "\nChapter 1\n\n", True)
+            out.append(image_prompt(styles[(step + j) % len(styles)], text, "A {style} style piece depicting the following: "))
+        return out
+
+    H = spec.resolution
+    gather_buf = None
+
+    def one_step(step: int):
+        nonlocal gather_buf
+        prompts = room_prompts(step)
+        seeds = [1000 * rank + 10 * step + j for j in range(args.batch)]
+        img = sd.generate_tensor(prompts, negative, seeds, steps=args.denoise_steps, scheduler=args.scheduler)
+        if world > 1:
+            if gather_buf is None:
+                gather_buf = [torch.empty_like(img) for _ in range(world)]
+            dist.all_gather(gather_buf, img.contiguous())
+        return img
+
+    for w in range(args.warmup):
+        one_step(w)
+    torch.cuda.synchronize(device) if device.type == "cuda" else None
+    if world > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        img = one_step(args.warmup + k)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    finite = bool(torch.isfinite(img.float()).all().item())
+
+    score = {}
+    if rank == 0 and not args.no_score:
+        from cassmantle_amd.scoring.encoder import EncoderBackend
+        from cassmantle_amd.game.scoring import score_pairs
+        be = EncoderBackend(device=str(device))
+        words = ["lantern", "river", "ancient", "glowing", "shadow", "ember", "crimson", "tower"]
+        pairs = [(words[i % 8], words[(i * 3 + 1) % 8]) for i in range(64)]
+        for _ in range(5):
+            score_pairs(be, pairs, 0.01)
+        lat = []
+        for _ in range(50):
+            t1 = time.perf_counter()
+            score_pairs(be, pairs, 0.01)
+            lat.append((time.perf_counter() - t1) * 1e3)
+        score = {"p50_score_ms": float(np.percentile(lat, 50)), "p99_score_ms": float(np.percentile(lat, 99)),
+                 "score_batch": len(pairs)}
+
+    if rank == 0:
+        images = world * args.batch * args.steps
+        value = images / elapsed
+        out = {
+            "metric": "SD-1.5 512^2 50-step images/sec (whole node) + p50 guess-score latency",
+            "value": round(value, 4),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_IMAGES_PER_SEC) if BASELINE_IMAGES_PER_SEC else None,
+            "dtype": "bf16",
+            "data": "synthetic (seeds.txt template prompts, random-init weights)",
+            "config": {"model": f"{args.model} UNet/VAE/CLIP-L ({spec.resolution}x{spec.resolution}, "
+                                f"{args.denoise_steps} steps {args.scheduler}, cfg 7.5)",
+                       "global_batch": world * args.batch, "seq_len": (spec.resolution // 8) ** 2,
+                       "parallelism": f"dp{world} (rooms)"},
+            "ops": "torch-eager" if args.baseline else "hip",
+            "graphs": bool(sd.use_graphs),
+            "finite": finite,
+            "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
+            **score,
+        }
+        print(json.dumps(out), flush=True)
+    cdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

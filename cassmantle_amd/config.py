@@ -1,0 +1,156 @@
+"""Typed configuration for the whole framework.
+
+The reference hard-codes every knob in constructor defaults:
+``main.py:23`` (round length 900 s), ``src/server.py:15-24`` (min_score 0.01),
+``src/backend.py:20-50`` (retries, lock timeouts, masks per prompt, episodes per story),
+``src/server.py:162`` (buffer trigger at 0.7 T), ``src/backend.py:319`` (blur range),
+``main.py:19,43,48,82,96,114`` (rate limits).  Here they live in one dataclass with the same
+defaults, overridable from the environment (``CASSMANTLE_<FIELD>``) or a CLI ``--key value``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, List, Optional, Sequence
+
+_ENV_PREFIX = "CASSMANTLE_"
+
+
+def _coerce(value: str, typ: Any) -> Any:
+    if typ in (bool, "bool"):
+        return value.strip().lower() in ("1", "true", "yes", "on")
+    if typ in (int, "int"):
+        return int(value)
+    if typ in (float, "float"):
+        return float(value)
+    if typ in (str, "str"):
+        return value
+    if typ in ("Optional[str]",):
+        return None if value.lower() in ("", "none", "null") else value
+    if typ in ("Optional[int]",):
+        return None if value.lower() in ("", "none", "null") else int(value)
+    # lists / dicts as JSON
+    return json.loads(value)
+
+
+@dataclass
+class GameConfig:
+    # --- round / scoring rules (reference defaults in effect) ---
+    time_per_prompt: int = 900            # main.py:23 (Server default 600 overridden)
+    min_score: float = 0.01               # src/server.py:17
+    max_retries: int = 5                  # src/backend.py:23
+    lock_timeout: float = 120.0           # src/backend.py:47
+    acquire_timeout: float = 2.0          # src/backend.py:48
+    num_masked: int = 2                   # src/backend.py:49
+    episode_per_story: int = 20           # src/backend.py:50
+    buffer_trigger_frac: float = 0.7      # src/server.py:162
+    min_blur: float = 0.0                 # src/backend.py:319
+    max_blur: float = 15.0                # src/backend.py:319
+    chapter_header: str = "\nChapter 1\n\n"   # src/backend.py:80,91
+    negative_prompt: str = "blurry, distorted, fake, abstract, negative"  # src/backend.py:284
+    style_template: str = "A {style} style piece depicting the following: "  # src/backend.py:272
+    llm_min_new_tokens: int = 32          # src/backend.py:252
+    llm_max_new_tokens: int = 96          # src/backend.py:253
+    # Quirk decisions.  True = keep reference behaviour.
+    quirk_exact_second_trigger: bool = False   # C.8: exact-second equality can miss; we use a latch
+    quirk_duplicate_masks: bool = False        # C.4: words.index() duplicates; we pick distinct indices
+    quirk_reset_story_on_restart: bool = False # C.9: restart re-inits story even if content exists
+    quirk_validate_indices: bool = True        # C.3: reject indices that are not masks (False = reference)
+    blur_bucket: float = 0.25             # per-score-bucket blur cache granularity (C.13 fix)
+    jpeg_quality: int = 75                # PIL default quality (src/utils.py:14)
+    # --- API ---
+    rate_default: str = "3/second"        # main.py:19
+    rate_root: str = "3/second"           # main.py:43
+    rate_game: str = "2/second"           # main.py:48,82,96,114
+    rate_limit_enabled: bool = True
+    clock_period: float = 1.0             # main.py:63
+    metrics_enabled: bool = False
+    num_rooms: int = 1
+    snapshot_path: Optional[str] = None   # JSON snapshot at round boundaries
+
+
+@dataclass
+class ModelConfig:
+    # --- on-device generation (BASELINE.json configs) ---
+    image_model: str = "sd15"            # sd15 | sdxl | tiny | solid
+    resolution: int = 512
+    steps: int = 50
+    guidance_scale: float = 7.5
+    scheduler: str = "pndm"               # pndm | ddim | euler
+    images_per_room: int = 1
+    dtype: str = "bf16"
+    device: str = "auto"                  # auto | cpu | cuda
+    use_graphs: bool = True               # hipGraph-captured denoise loop
+    fp8_attention: bool = False           # BASELINE config 4 (SDXL)
+    weights_path: Optional[str] = None    # optional safetensors checkpoint dir
+    seed: int = 0
+    scorer: str = "minilm"               # minilm | wordvec
+    scorer_batch_window_ms: float = 1.0   # micro-batch window for streaming guess scoring
+    prompt_generator: str = "synthetic"   # synthetic | lm
+
+
+@dataclass
+class Config:
+    game: GameConfig = field(default_factory=GameConfig)
+    model: ModelConfig = field(default_factory=ModelConfig)
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def _apply(obj: Any, key: str, raw: str) -> bool:
+        for f in fields(obj):
+            if f.name == key:
+                setattr(obj, key, _coerce(raw, f.type))
+                return True
+        return False
+
+    def set(self, key: str, raw: str) -> None:
+        key = key.replace("-", "_")
+        if "." in key:
+            sect, sub = key.split(".", 1)
+            if not self._apply(getattr(self, sect), sub, raw):
+                raise KeyError(key)
+            return
+        if not (self._apply(self.game, key, raw) or self._apply(self.model, key, raw)):
+            raise KeyError(key)
+
+    @classmethod
+    def from_env(cls, environ: Optional[Dict[str, str]] = None) -> "Config":
+        cfg = cls()
+        env = os.environ if environ is None else environ
+        for k, v in env.items():
+            if k.startswith(_ENV_PREFIX):
+                try:
+                    cfg.set(k[len(_ENV_PREFIX):].lower(), v)
+                except KeyError:
+                    pass
+        return cfg
+
+    @classmethod
+    def from_args(cls, argv: Sequence[str], base: Optional["Config"] = None) -> "Config":
+        cfg = base or cls.from_env()
+        it = iter(list(argv))
+        for tok in it:
+            if not tok.startswith("--"):
+                continue
+            tok = tok[2:]
+            if "=" in tok:
+                k, v = tok.split("=", 1)
+            else:
+                k, v = tok, next(it, "true")
+            cfg.set(k, v)
+        return cfg
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+
+def parse_rate(rate: str) -> tuple:
+    """'3/second' -> (3, 1.0).  Accepts second/minute/hour (slowapi syntax subset)."""
+    n, per = rate.split("/")
+    per = per.strip().lower()
+    unit = {"second": 1.0, "s": 1.0, "minute": 60.0, "m": 60.0, "hour": 3600.0, "h": 3600.0}
+    if per not in unit:
+        raise ValueError(f"bad rate {rate}")
+    return int(n), unit[per]

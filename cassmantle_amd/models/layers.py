@@ -1,0 +1,134 @@
+"""NHWC building blocks for the diffusion / text models, routed through ``cassmantle_amd.ops``.
+
+Design (MI355X-first):
+* activations NHWC bf16, so every conv is an implicit GEMM with K-contiguous operands and a
+  transformer's ``[B, H*W, C]`` token view is free (no permutes around attention blocks);
+* Q/K/V projections are one fused ``[3C, C]`` GEMM; the attention kernel reads Q/K/V as
+  strided views of its output (no split/transposes);
+* bias, residual adds, GEGLU, SiLU/GELU and the ResNet time-embedding add are GEMM/conv
+  epilogues; GroupNorm+SiLU is one kernel.
+
+Module names follow the diffusers/transformers parameter naming so a real checkpoint can be
+mapped in (``models/weights.py``); weights are random-init by default (BASELINE.json).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+def _param(shape, std, gen: Optional[torch.Generator], dtype) -> nn.Parameter:
+    t = torch.randn(*shape, generator=gen, dtype=torch.float32) * std
+    return nn.Parameter(t.to(dtype), requires_grad=False)
+
+
+def _zeros(shape, dtype) -> nn.Parameter:
+    return nn.Parameter(torch.zeros(*shape, dtype=dtype), requires_grad=False)
+
+
+def _ones(shape, dtype) -> nn.Parameter:
+    return nn.Parameter(torch.ones(*shape, dtype=dtype), requires_grad=False)
+
+
+class Linear(nn.Module):
+    def __init__(self, fin: int, fout: int, bias: bool = True, gen=None, dtype=torch.bfloat16,
+                 std: Optional[float] = None):
+        super().__init__()
+        self.fin, self.fout = fin, fout
+        self.weight = _param((fout, fin), std if std is not None else 1.0 / math.sqrt(fin), gen, dtype)
+        self.bias = _param((fout,), 0.02, gen, dtype) if bias else None
+
+    def forward(self, x, residual=None, act=None):
+        return ops.linear(x, self.weight, self.bias, residual=residual, act=act)
+
+
+class Conv2d(nn.Module):
+    """NHWC conv; weight [Cout, kh, kw, Cin]."""
+
+    def __init__(self, cin: int, cout: int, k: int = 3, stride: int = 1, padding: Optional[int] = None,
+                 bias: bool = True, gen=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.padding = (k // 2) if padding is None else padding
+        self.weight = _param((cout, k, k, cin), 1.0 / math.sqrt(cin * k * k), gen, dtype)
+        self.bias = _param((cout,), 0.02, gen, dtype) if bias else None
+
+    def forward(self, x, residual=None, upsample=False, chan_bias=None):
+        if self.k == 1 and self.stride == 1 and not upsample and chan_bias is None:
+            return ops.linear(x, self.weight.view(self.cout, self.cin), self.bias, residual=residual)
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, residual=residual,
+                          upsample=upsample, chan_bias=chan_bias)
+
+
+class GroupNorm(nn.Module):
+    def __init__(self, groups: int, channels: int, eps: float = 1e-5, dtype=torch.bfloat16):
+        super().__init__()
+        self.groups, self.eps = groups, eps
+        self.weight = _ones((channels,), dtype)
+        self.bias = _zeros((channels,), dtype)
+
+    def forward(self, x, silu=False):
+        return ops.group_norm(x, self.groups, self.weight, self.bias, self.eps, silu)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5, dtype=torch.bfloat16):
+        super().__init__()
+        self.eps = eps
+        self.weight = _ones((dim,), dtype)
+        self.bias = _zeros((dim,), dtype)
+
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class SelfAttention(nn.Module):
+    """Multi-head self attention with fused QKV projection; output projection fuses the
+    residual add."""
+
+    def __init__(self, dim: int, heads: int, gen=None, dtype=torch.bfloat16, qkv_bias=False,
+                 out_bias=True):
+        super().__init__()
+        self.dim, self.heads = dim, heads
+        self.head_dim = dim // heads
+        self.to_qkv = Linear(dim, 3 * dim, bias=qkv_bias, gen=gen, dtype=dtype)
+        self.to_out = Linear(dim, dim, bias=out_bias, gen=gen, dtype=dtype)
+
+    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False):
+        B, N, C = x.shape
+        qkv = self.to_qkv(x).view(B, N, 3, self.heads, self.head_dim)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, kv_lens=kv_lens, fp8=fp8)
+        return self.to_out(o.reshape(B, N, C), residual=residual)
+
+
+class CrossAttention(nn.Module):
+    def __init__(self, dim: int, ctx_dim: int, heads: int, gen=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.dim, self.heads = dim, heads
+        self.head_dim = dim // heads
+        self.to_q = Linear(dim, dim, bias=False, gen=gen, dtype=dtype)
+        self.to_kv = Linear(ctx_dim, 2 * dim, bias=False, gen=gen, dtype=dtype)
+        self.to_out = Linear(dim, dim, bias=True, gen=gen, dtype=dtype)
+
+    def forward(self, x, ctx, residual=None, fp8=False):
+        B, N, C = x.shape
+        q = self.to_q(x).view(B, N, self.heads, self.head_dim)
+        kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, self.heads, self.head_dim)
+        o = ops.attention(q, kv[:, :, 0], kv[:, :, 1], fp8=fp8)
+        return self.to_out(o.reshape(B, N, C), residual=residual)
+
+
+class GEGLUFeedForward(nn.Module):
+    def __init__(self, dim: int, mult: int = 4, gen=None, dtype=torch.bfloat16):
+        super().__init__()
+        inner = dim * mult
+        self.proj_in = Linear(dim, 2 * inner, gen=gen, dtype=dtype)  # [value; gate] rows
+        self.proj_out = Linear(inner, dim, gen=gen, dtype=dtype)
+
+    def forward(self, x, residual=None):
+        return self.proj_out(self.proj_in(x, act="geglu"), residual=residual)

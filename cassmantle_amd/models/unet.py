@@ -1,0 +1,233 @@
+"""UNet2DCondition (SD-1.5 and SDXL configurations), NHWC, on ``cassmantle_amd.ops``.
+
+Implied by the reference's remote txt2img call (``src/backend.py:270-295``; SURVEY §2.3,
+kernels K1/K2/K4/K6–K12).  Architecture per the public SD-1.5 / SDXL-base UNet configs
+[ext]: ResNet blocks (GroupNorm+SiLU → 3×3 conv, time-embedding add, GroupNorm+SiLU →
+3×3 conv, shortcut), spatial transformers (GroupNorm → proj_in → [LN → self-attn → LN →
+cross-attn → LN → GEGLU FF] × depth → proj_out + residual), stride-2 conv downsamplers,
+nearest-2× upsample fused into the following conv, skip concatenation on the channel axis.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import (Conv2d, CrossAttention, GEGLUFeedForward, GroupNorm, LayerNorm, Linear,
+                     SelfAttention)
+
+
+@dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: Tuple[int, ...] = (320, 640, 1280, 1280)
+    # per level: does the down block have cross-attn transformers, and how deep
+    down_attn: Tuple[bool, ...] = (True, True, True, False)
+    transformer_depth: Tuple[int, ...] = (1, 1, 1, 1)
+    mid_transformer_depth: int = 1
+    layers_per_block: int = 2
+    heads: Tuple[int, ...] = (8, 8, 8, 8)           # SD-1.5: 8 heads everywhere (head_dim 40/80/160)
+    head_dim: Optional[int] = None                  # SDXL: fixed 64 (heads = C / 64)
+    cross_attention_dim: int = 768
+    norm_groups: int = 32
+    norm_eps: float = 1e-5
+    transformer_norm_eps: float = 1e-6
+    time_proj_dim: int = 320
+    time_embed_dim: int = 1280
+    linear_projection: bool = False
+    addition_embed: bool = False                    # SDXL text_time add-embeds
+    addition_time_embed_dim: int = 256
+    projection_class_embeddings_input_dim: int = 2816
+    sample_size: int = 64
+
+    def level_heads(self, i: int) -> int:
+        if self.head_dim is not None:
+            return self.block_out_channels[i] // self.head_dim
+        return self.heads[i]
+
+
+SD15_UNET = UNetConfig()
+SDXL_UNET = UNetConfig(block_out_channels=(320, 640, 1280), down_attn=(False, True, True),
+                       transformer_depth=(0, 2, 10), mid_transformer_depth=10, heads=(5, 10, 20),
+                       head_dim=64, cross_attention_dim=2048, linear_projection=True,
+                       addition_embed=True, sample_size=128)
+TINY_UNET = UNetConfig(block_out_channels=(32, 64), down_attn=(True, False), transformer_depth=(1, 1),
+                       heads=(2, 2), layers_per_block=1, cross_attention_dim=32, norm_groups=8,
+                       time_proj_dim=32, time_embed_dim=64, sample_size=8)
+
+
+class ResnetBlock(nn.Module):
+    def __init__(self, cin: int, cout: int, temb: int, groups: int, eps: float, gen, dtype):
+        super().__init__()
+        self.norm1 = GroupNorm(groups, cin, eps, dtype)
+        self.conv1 = Conv2d(cin, cout, 3, gen=gen, dtype=dtype)
+        self.time_emb_proj = Linear(temb, cout, gen=gen, dtype=dtype)
+        self.norm2 = GroupNorm(groups, cout, eps, dtype)
+        self.conv2 = Conv2d(cout, cout, 3, gen=gen, dtype=dtype)
+        self.conv_shortcut = Conv2d(cin, cout, 1, padding=0, gen=gen, dtype=dtype) if cin != cout else None
+
+    def forward(self, x, temb_silu):
+        h = self.norm1(x, silu=True)
+        tb = self.time_emb_proj(temb_silu)                       # [B, cout]
+        h = self.conv1(h, chan_bias=tb)                          # time-emb add fused in epilogue
+        h = self.norm2(h, silu=True)
+        sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        return self.conv2(h, residual=sc)                        # residual fused in epilogue
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, ctx_dim: int, gen, dtype):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, 1e-5, dtype)
+        self.attn1 = SelfAttention(dim, heads, gen=gen, dtype=dtype)
+        self.norm2 = LayerNorm(dim, 1e-5, dtype)
+        self.attn2 = CrossAttention(dim, ctx_dim, heads, gen=gen, dtype=dtype)
+        self.norm3 = LayerNorm(dim, 1e-5, dtype)
+        self.ff = GEGLUFeedForward(dim, 4, gen=gen, dtype=dtype)
+
+    def forward(self, x, ctx, fp8=False):
+        x = self.attn1(self.norm1(x), residual=x, fp8=fp8)
+        x = self.attn2(self.norm2(x), ctx, residual=x, fp8=fp8)
+        x = self.ff(self.norm3(x), residual=x)
+        return x
+
+
+class Transformer2D(nn.Module):
+    def __init__(self, dim: int, heads: int, depth: int, ctx_dim: int, groups: int, gen, dtype):
+        super().__init__()
+        self.norm = GroupNorm(groups, dim, 1e-6, dtype)
+        self.proj_in = Linear(dim, dim, gen=gen, dtype=dtype)    # 1x1 conv == linear in NHWC
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(dim, heads, ctx_dim, gen, dtype) for _ in range(depth)])
+        self.proj_out = Linear(dim, dim, gen=gen, dtype=dtype)
+
+    def forward(self, x, ctx, fp8=False):
+        B, H, W, C = x.shape
+        h = self.norm(x).view(B, H * W, C)
+        h = self.proj_in(h)
+        for blk in self.transformer_blocks:
+            h = blk(h, ctx, fp8=fp8)
+        return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
+
+
+class Downsample(nn.Module):
+    def __init__(self, c: int, gen, dtype):
+        super().__init__()
+        self.conv = Conv2d(c, c, 3, stride=2, padding=1, gen=gen, dtype=dtype)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample(nn.Module):
+    def __init__(self, c: int, gen, dtype):
+        super().__init__()
+        self.conv = Conv2d(c, c, 3, gen=gen, dtype=dtype)
+
+    def forward(self, x):
+        return self.conv(x, upsample=True)                       # nearest-2x fused into conv
+
+
+class UNet(nn.Module):
+    def __init__(self, cfg: UNetConfig = SD15_UNET, seed: int = 0, dtype=torch.bfloat16):
+        super().__init__()
+        self.cfg = cfg
+        gen = torch.Generator().manual_seed(seed)
+        ch = cfg.block_out_channels
+        g, eps, te = cfg.norm_groups, cfg.norm_eps, cfg.time_embed_dim
+        self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, gen=gen, dtype=dtype)
+        self.time_linear_1 = Linear(cfg.time_proj_dim, te, gen=gen, dtype=dtype)
+        self.time_linear_2 = Linear(te, te, gen=gen, dtype=dtype)
+        if cfg.addition_embed:
+            self.add_linear_1 = Linear(cfg.projection_class_embeddings_input_dim, te, gen=gen, dtype=dtype)
+            self.add_linear_2 = Linear(te, te, gen=gen, dtype=dtype)
+        self.down = nn.ModuleList()
+        skip_ch: List[int] = [ch[0]]
+        cur = ch[0]
+        n = len(ch)
+        for i in range(n):
+            blk = nn.Module()
+            blk.resnets = nn.ModuleList()
+            blk.attentions = nn.ModuleList()
+            for j in range(cfg.layers_per_block):
+                blk.resnets.append(ResnetBlock(cur, ch[i], te, g, eps, gen, dtype))
+                cur = ch[i]
+                if cfg.down_attn[i]:
+                    blk.attentions.append(Transformer2D(cur, cfg.level_heads(i), cfg.transformer_depth[i],
+                                                       cfg.cross_attention_dim, g, gen, dtype))
+                skip_ch.append(cur)
+            blk.downsampler = Downsample(cur, gen, dtype) if i < n - 1 else None
+            if i < n - 1:
+                skip_ch.append(cur)
+            self.down.append(blk)
+        self.mid_res1 = ResnetBlock(cur, cur, te, g, eps, gen, dtype)
+        self.mid_attn = Transformer2D(cur, cfg.level_heads(n - 1), cfg.mid_transformer_depth,
+                                      cfg.cross_attention_dim, g, gen, dtype)
+        self.mid_res2 = ResnetBlock(cur, cur, te, g, eps, gen, dtype)
+        self.up = nn.ModuleList()
+        rev = list(reversed(range(n)))
+        for ui, i in enumerate(rev):
+            blk = nn.Module()
+            blk.resnets = nn.ModuleList()
+            blk.attentions = nn.ModuleList()
+            for j in range(cfg.layers_per_block + 1):
+                sk = skip_ch.pop()
+                blk.resnets.append(ResnetBlock(cur + sk, ch[i], te, g, eps, gen, dtype))
+                cur = ch[i]
+                if cfg.down_attn[i]:
+                    blk.attentions.append(Transformer2D(cur, cfg.level_heads(i), cfg.transformer_depth[i],
+                                                       cfg.cross_attention_dim, g, gen, dtype))
+            blk.upsampler = Upsample(cur, gen, dtype) if ui < n - 1 else None
+            self.up.append(blk)
+        self.conv_norm_out = GroupNorm(g, cur, eps, dtype)
+        self.conv_out = Conv2d(cur, cfg.out_channels, 3, gen=gen, dtype=dtype)
+
+    # ------------------------------------------------------------------
+    def time_embed(self, t: torch.Tensor, added: Optional[dict] = None) -> torch.Tensor:
+        """Returns SiLU(temb) (every consumer applies SiLU first, so it is fused here)."""
+        tp = ops.timestep_embedding(t, self.cfg.time_proj_dim).to(self.time_linear_1.weight.dtype)
+        emb = self.time_linear_2(self.time_linear_1(tp, act="silu"))
+        if self.cfg.addition_embed and added is not None:
+            tid = added["time_ids"]                                  # [B, 6]
+            B = tid.shape[0]
+            te = ops.timestep_embedding(tid.reshape(-1), self.cfg.addition_time_embed_dim).reshape(B, -1)
+            a_in = torch.cat([added["text_embeds"].float(), te], dim=-1).to(emb.dtype)
+            emb = self.add_linear_2(self.add_linear_1(a_in, act="silu"), residual=emb)
+        return _silu(emb)
+
+    def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor,
+                added: Optional[dict] = None, fp8: bool = False) -> torch.Tensor:
+        """x [B, H, W, 4] NHWC, t [B] (float), ctx [B, 77, D] -> eps [B, H, W, 4]."""
+        temb = self.time_embed(t, added)
+        h = self.conv_in(x)
+        skips = [h]
+        for blk in self.down:
+            for j, res in enumerate(blk.resnets):
+                h = res(h, temb)
+                if len(blk.attentions):
+                    h = blk.attentions[j](h, ctx, fp8)
+                skips.append(h)
+            if blk.downsampler is not None:
+                h = blk.downsampler(h)
+                skips.append(h)
+        h = self.mid_res1(h, temb)
+        h = self.mid_attn(h, ctx, fp8)
+        h = self.mid_res2(h, temb)
+        for blk in self.up:
+            for j, res in enumerate(blk.resnets):
+                h = torch.cat([h, skips.pop()], dim=-1)
+                h = res(h, temb)
+                if len(blk.attentions):
+                    h = blk.attentions[j](h, ctx, fp8)
+            if blk.upsampler is not None:
+                h = blk.upsampler(h)
+        h = self.conv_norm_out(h, silu=True)
+        return self.conv_out(h)
+
+
+def _silu(x: torch.Tensor) -> torch.Tensor:
+    return torch.nn.functional.silu(x.float()).to(x.dtype)

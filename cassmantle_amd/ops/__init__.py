@@ -1,0 +1,275 @@
+"""Op dispatch: hand-written HIP/CDNA4 kernels on the GPU, PyTorch reference on the CPU.
+
+Every hot op of the SD pipeline and the scorer (SURVEY §2.3 kernel inventory K1–K18) is a
+function here.  On a ROCm device tensor the call goes to the in-tree extension
+``cassmantle_amd/_C*.so`` (built by ``cassmantle_amd/build.py`` with ``hipcc
+--offload-arch=gfx950``); if that extension is missing on a GPU box the op **raises** — there
+is no silent eager fallback.  ``CASSMANTLE_OPS=torch`` is an explicit opt-in to the stock
+PyTorch ops (used only by ``bench.py --baseline`` to measure the vendor-library baseline).
+CPU tensors always run ``ops.reference``.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._ext import ext, ext_available, ext_error
+
+_MODE = os.environ.get("CASSMANTLE_OPS", "hip").lower()
+
+
+def set_mode(mode: str) -> None:
+    global _MODE
+    assert mode in ("hip", "torch")
+    _MODE = mode
+
+
+def get_mode() -> str:
+    return _MODE
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    if t.device.type != "cuda":
+        return False
+    if _MODE == "torch":
+        return False
+    if not ext_available():
+        raise RuntimeError(
+            "cassmantle_amd HIP extension is not loaded on a GPU device "
+            f"({ext_error()}); run `python -m cassmantle_amd.build` or set CASSMANTLE_OPS=torch "
+            "explicitly for the stock-PyTorch baseline")
+    return True
+
+
+_ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5}
+
+
+# ----------------------------------------------------------------------------- GEMM (K6)
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           residual: Optional[torch.Tensor] = None, act: Optional[str] = None) -> torch.Tensor:
+    """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu)."""
+    if not _use_hip(x):
+        if x.device.type == "cuda":  # explicit torch baseline mode: stock ops in bf16
+            return _torch_linear(x, w, bias, residual, act)
+        return ref.linear(x, w, bias, residual, act)
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    N = w.shape[0] // 2 if act == "geglu" else w.shape[0]
+    out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    ext().gemm(x2, w, bias, r2, out, _ACT[act])
+    return out.reshape(*x.shape[:-1], N)
+
+
+def _torch_linear(x, w, bias, residual, act):
+    import torch.nn.functional as F
+    y = F.linear(x, w, bias)
+    if act == "geglu":
+        h, g = y.chunk(2, dim=-1)
+        y = h * F.gelu(g)
+    elif act == "gelu":
+        y = F.gelu(y)
+    elif act == "gelu_tanh":
+        y = F.gelu(y, approximate="tanh")
+    elif act == "silu":
+        y = F.silu(y)
+    elif act == "quick_gelu":
+        y = y * torch.sigmoid(1.702 * y)
+    if residual is not None:
+        y = y + residual
+    return y
+
+
+# ----------------------------------------------------------------------------- conv (K4/K5/K12)
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+           padding: int = 1, residual: Optional[torch.Tensor] = None, upsample: bool = False,
+           chan_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NHWC implicit-GEMM convolution.  x [B,H,W,Cin], w [Cout,kh,kw,Cin]."""
+    if not _use_hip(x):
+        if x.device.type == "cuda":
+            return _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias)
+        return ref.conv2d(x, w, bias, stride, padding, residual, upsample, chan_bias)
+    B, H, W, Cin = x.shape
+    Cout, kh, kw, _ = w.shape
+    Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
+    Ho = (Hi + 2 * padding - kh) // stride + 1
+    Wo = (Wi + 2 * padding - kw) // stride + 1
+    out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=x.dtype)
+    ext().conv2d(x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample))
+    return out
+
+
+def _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias):
+    import torch.nn.functional as F
+    xi = x.permute(0, 3, 1, 2)
+    if upsample:
+        xi = F.interpolate(xi, scale_factor=2.0, mode="nearest")
+    wi = w.permute(0, 3, 1, 2)
+    y = F.conv2d(xi.contiguous(memory_format=torch.channels_last),
+                 wi.contiguous(memory_format=torch.channels_last), bias, stride=stride, padding=padding)
+    y = y.permute(0, 2, 3, 1)
+    if chan_bias is not None:
+        y = y + chan_bias[:, None, None, :]
+    if residual is not None:
+        y = y + residual
+    return y.contiguous()
+
+
+# ----------------------------------------------------------------------------- norms (K7/K8)
+def group_norm(x: torch.Tensor, num_groups: int, weight: torch.Tensor, bias: torch.Tensor,
+               eps: float, silu: bool = False) -> torch.Tensor:
+    if not _use_hip(x):
+        if x.device.type == "cuda":
+            import torch.nn.functional as F
+            B, C = x.shape[0], x.shape[-1]
+            xi = x.reshape(B, -1, C).transpose(1, 2)
+            y = F.group_norm(xi, num_groups, weight, bias, eps)
+            if silu:
+                y = F.silu(y)
+            return y.transpose(1, 2).reshape(x.shape).contiguous()
+        return ref.group_norm(x, num_groups, weight, bias, eps, silu)
+    out = torch.empty_like(x)
+    ext().group_norm(x.contiguous(), weight, bias, out, num_groups, float(eps), int(silu))
+    return out
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float) -> torch.Tensor:
+    if not _use_hip(x):
+        if x.device.type == "cuda":
+            import torch.nn.functional as F
+            return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+        return ref.layer_norm(x, weight, bias, eps)
+    out = torch.empty_like(x)
+    ext().layer_norm(x.contiguous(), weight, bias, out, float(eps))
+    return out
+
+
+# ----------------------------------------------------------------------------- attention (K1/K2/K3)
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,
+              causal: bool = False, kv_lens: Optional[torch.Tensor] = None,
+              fp8: bool = False) -> torch.Tensor:
+    """Flash attention.  q [B,Nq,H,d], k/v [B,Nk,H,d]; strided views allowed (last dim
+    contiguous), e.g. slices of a fused QKV projection output.  Returns [B,Nq,H,d]."""
+    d = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(d)
+    if not _use_hip(q):
+        if q.device.type == "cuda":
+            import torch.nn.functional as F
+            mask = None
+            if kv_lens is not None:
+                ar = torch.arange(k.shape[1], device=q.device)
+                mask = (ar[None, :] < kv_lens[:, None])[:, None, None, :]
+            o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                               attn_mask=mask, is_causal=causal and mask is None, scale=scale)
+            return o.transpose(1, 2)
+        return ref.attention(q, k, v, scale, causal, kv_lens)
+    B, Nq, H, _ = q.shape
+    if d > 256:
+        return _attention_gemm(q, k, v, scale, causal, kv_lens)
+    out = torch.empty((B, Nq, H, d), device=q.device, dtype=q.dtype)
+    ext().attention(q, k, v, out, float(scale), int(causal), kv_lens, int(fp8))
+    return out
+
+
+def _attention_gemm(q, k, v, scale, causal, kv_lens):
+    """Large head dim (VAE mid-block, d=512, single head): S = QK^T on MFMA GEMM, fused
+    row-softmax kernel, O = PV.  S fits HBM trivially ([B,4096,4096] fp32 = 64 MB/img)."""
+    B, Nq, H, d = q.shape
+    outs = []
+    for h in range(H):
+        qh, kh, vh = q[:, :, h], k[:, :, h], v[:, :, h]
+        s = torch.empty((B, Nq, k.shape[1]), device=q.device, dtype=torch.float32)
+        ext().bmm_nt(qh, kh, s, float(scale))
+        p = torch.empty((B, Nq, k.shape[1]), device=q.device, dtype=q.dtype)
+        ext().softmax_rows(s, p, int(causal), kv_lens)
+        o = torch.empty((B, Nq, d), device=q.device, dtype=q.dtype)
+        vt = vh.transpose(1, 2).contiguous()  # [B, d, Nk] K-contiguous for the NT GEMM
+        ext().bmm_nt(p, vt, o, 1.0)
+        outs.append(o)
+    return torch.stack(outs, dim=2)
+
+
+# ----------------------------------------------------------------------------- scorer (K14/K15/K16)
+def gather_cosine(table: torch.Tensor, ia: torch.Tensor, ib: torch.Tensor) -> torch.Tensor:
+    if not _use_hip(table):
+        return ref.gather_cosine(table, ia, ib)
+    out = torch.empty(ia.shape[0], device=table.device, dtype=torch.float32)
+    ext().gather_cosine(table, ia.int().contiguous(), ib.int().contiguous(), out)
+    return out
+
+
+def pair_cosine(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if not _use_hip(a):
+        return ref.pair_cosine(a, b)
+    out = torch.empty(a.shape[0], device=a.device, dtype=torch.float32)
+    ext().pair_cosine(a.contiguous(), b.contiguous(), out)
+    return out
+
+
+def cosine_topk(table: torch.Tensor, vec: torch.Tensor, k: int):
+    if not _use_hip(table):
+        return ref.cosine_topk(table, vec, k)
+    s = torch.empty(table.shape[0], device=table.device, dtype=torch.float32)
+    ext().cosine_gemv(table, vec.contiguous(), s)
+    return torch.topk(s, k)
+
+
+def mean_pool_l2(hidden: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+    if not _use_hip(hidden):
+        return ref.mean_pool_l2(hidden, lens)
+    out = torch.empty((hidden.shape[0], hidden.shape[-1]), device=hidden.device, dtype=torch.float32)
+    ext().mean_pool_l2(hidden.contiguous(), lens.int().contiguous(), out)
+    return out
+
+
+# ----------------------------------------------------------------------------- image (K17/K18)
+def gaussian_blur(img: torch.Tensor, sigma: float) -> torch.Tensor:
+    if not _use_hip(img) or sigma <= 0:
+        return ref.gaussian_blur(img, sigma)
+    w = ref.gaussian_kernel1d(sigma, img.device)
+    out = torch.empty_like(img)
+    ext().gaussian_blur(img.contiguous(), w, out)
+    return out
+
+
+def vae_postprocess(x: torch.Tensor) -> torch.Tensor:
+    """[B,H,W,3] in [-1,1] -> uint8 [B,H,W,3] (clamp((x+1)/2)*255, round)."""
+    if not _use_hip(x):
+        return ((x.float() / 2 + 0.5).clamp(0, 1) * 255.0).round().to(torch.uint8)
+    out = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+    ext().to_uint8(x.contiguous(), out)
+    return out
+
+
+# ----------------------------------------------------------------------------- diffusion glue (K10/K11)
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
+    if not _use_hip(t):
+        return ref.timestep_embedding(t, dim, flip_sin_to_cos, shift)
+    out = torch.empty((t.shape[0], dim), device=t.device, dtype=torch.float32)
+    ext().timestep_embedding(t.float().contiguous(), out, int(flip_sin_to_cos), float(shift))
+    return out
+
+
+def latent_step(eps: torch.Tensor, x: torch.Tensor, hist: torch.Tensor, xs: torch.Tensor,
+                coef: torch.Tensor, step: torch.Tensor, unet_in: torch.Tensor, cfg: bool) -> None:
+    """Fused CFG-combine + scheduler update + next-step UNet-input write (see
+    ``models/schedulers.py`` for the coefficient-table contract).  In place on x/hist/xs/unet_in.
+    ``step`` is a device int32 scalar so the whole step is graph-capturable."""
+    if not _use_hip(x):
+        from ..models.schedulers import latent_step_reference
+        latent_step_reference(eps, x, hist, xs, coef, step, unet_in, cfg)
+        return
+    ext().latent_step(eps, x, hist, xs, coef, step, unet_in, int(cfg))
+
+
+def advance_step(step: torch.Tensor) -> None:
+    if not _use_hip(step):
+        step.add_(1)
+        return
+    ext().advance_step(step)
