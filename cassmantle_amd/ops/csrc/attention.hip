@@ -1,0 +1,298 @@
+// Flash-attention forward for gfx950 (SURVEY §2.3 K1 self-attn, K2 cross-attn, K13/K16 text
+// encoders): softmax(Q K^T * scale) V with online softmax, no score matrix in HBM.
+//
+// MFMA formulation (v_mfma_f32_32x32x16_bf16), chosen so every softmax quantity is lane-local:
+//   S^T[key][q] = K[key][:] . Q[q][:]      A = K tile from LDS (ds_read_b128 rows),
+//                                          B = Q^T fragments held in registers for the whole loop
+//   -> each lane owns ONE query column (q = lane & 31) and 16 of the tile's keys; the other 16
+//      keys of that query sit in lane ^ 32, so a row max / row sum is 31 VALU ops + one
+//      cross-half shuffle (cdna_hip_programming.md Appendix B 'swapped QK^T').
+//   O^T[d][q] += V^T[d][key] . P^T[key][q]  B = P^T taken straight from the S^T accumulator
+//                                           registers (converted to bf16, permuted k order;
+//                                           guide §3 'accumulator tile as next MFMA operand'),
+//                                           A = V^T via ds_read_b64_tr_b16 hardware-transposed
+//                                           LDS reads of the row-major V tile (T10).
+//   -> the O accumulator is also query-per-lane, so the online-softmax rescale and the final
+//      1/l normalisation are lane-local multiplies.
+// Head dims 40/80/160 (SD-1.5), 64 (SDXL, CLIP), 32 (MiniLM): QK^T runs over d padded to 16,
+// P.V over d padded to 32; padding is zero-filled in LDS.  Ragged key counts (77-token cross
+// attention, padded MiniLM batches via kv_lens) and causal masking (CLIP) are masked to -inf.
+// K/V tiles of 64 keys are staged global->registers->LDS with the next tile's loads issued
+// before the current tile's MFMAs (T14).  LDS strides are padded so the K row reads
+// (16 distinct rows per lane group) and the V transposed reads are bank-conflict-free.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int KT = 64;  // keys per tile
+
+template <int DQK, int DO>
+struct AttnGeom {
+  static constexpr int KCH = DQK / 8;                         // 16B chunks per K row
+  static constexpr int KSTR = (KCH % 2 == 0 ? KCH + 1 : KCH) * 8;  // elements; odd chunk count
+  static constexpr int VCH = DO / 8;
+  static constexpr int VB = DO * 2;                            // bytes per V row
+  static constexpr int VSTR = ((VB % 256 == 64) || (VB % 256 == 192)) ? DO : DO + 32;
+  static constexpr int LDS_BYTES = KT * KSTR * 2 + KT * VSTR * 2;
+};
+
+template <int DQK, int DO, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
+  using G = AttnGeom<DQK, DO>;
+  constexpr int THREADS = 64 * NW;
+  constexpr int QB = 32 * NW;
+  constexpr int NKS = DQK / 16;       // k-steps of QK^T
+  constexpr int NDC = DO / 32;        // 32-row chunks of O^T
+  constexpr int KLD = (KT * G::KCH + THREADS - 1) / THREADS;
+  constexpr int VLD = (KT * G::VCH + THREADS - 1) / THREADS;
+
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Ks = lds;
+  uint16_t* Vs = lds + KT * G::KSTR;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hlf = lane >> 5;          // lane half
+  const int ql = lane & 31;
+
+  const int nqb = (a.Nq + QB - 1) / QB;
+  const int bid = blockIdx.x;
+  const int qb = bid % nqb;
+  const int bh = bid / nqb;
+  const int h = bh % a.H;
+  const int b = bh / a.H;
+  const int q0 = qb * QB + wave * 32;
+  const int q = q0 + ql;
+
+  int nk = a.Nk;
+  if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
+  int ntiles = (nk + KT - 1) / KT;
+  if (a.causal) ntiles = min(ntiles, (qb * QB + QB + KT - 1) / KT);
+
+  const uint16_t* Qp = a.q + (long long)b * a.q_sb + (long long)h * a.q_sh;
+  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)h * a.k_sh;
+  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)h * a.v_sh;
+  const int d = a.d;
+
+  // Q^T fragments: lane holds Q[q][ks*16 + 8*hlf .. +7]
+  bf16x8_t qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    int d0 = ks * 16 + 8 * hlf;
+    if (q < a.Nq && d0 < d) v = *reinterpret_cast<const uint4*>(Qp + (long long)q * a.q_sn + d0);
+    qf[ks] = as_bf16x8(v);
+  }
+
+  f32x16_t oacc[NDC];
+#pragma unroll
+  for (int i = 0; i < NDC; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+  const float c = a.scale * 1.4426950408889634f;
+
+  uint4 kr[KLD], vr[VLD];
+  auto gload = [&](int t) {
+    const int kbase = t * KT;
+#pragma unroll
+    for (int i = 0; i < KLD; ++i) {
+      int idx = tid + i * THREADS;
+      int key = idx / G::KCH, ch = idx - key * G::KCH;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (key < KT && kbase + key < nk && ch * 8 < d)
+        v = *reinterpret_cast<const uint4*>(Kp + (long long)(kbase + key) * a.k_sn + ch * 8);
+      kr[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < VLD; ++i) {
+      int idx = tid + i * THREADS;
+      int key = idx / G::VCH, ch = idx - key * G::VCH;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (key < KT && kbase + key < nk && ch * 8 < d)
+        v = *reinterpret_cast<const uint4*>(Vp + (long long)(kbase + key) * a.v_sn + ch * 8);
+      vr[i] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < KLD; ++i) {
+      int idx = tid + i * THREADS;
+      int key = idx / G::KCH, ch = idx - key * G::KCH;
+      if (key < KT) *reinterpret_cast<uint4*>(Ks + key * G::KSTR + ch * 8) = kr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VLD; ++i) {
+      int idx = tid + i * THREADS;
+      int key = idx / G::VCH, ch = idx - key * G::VCH;
+      if (key < KT) *reinterpret_cast<uint4*>(Vs + key * G::VSTR + ch * 8) = vr[i];
+    }
+  };
+
+  if (ntiles > 0) {
+    gload(0);
+    lstore();
+  }
+  __syncthreads();
+
+  // tr-read lane geometry (T10): group g = lane>>4, i = lane&15 -> row q' = i>>2, col 4*(i&3)
+  const int tg = lane >> 4, ti = lane & 15;
+  const int tr_row = 4 * (tg >> 1) + (ti >> 2);
+  const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = t + 1 < ntiles;
+    if (more) gload(t + 1);
+
+    // ---- S^T = K Q^T for 64 keys (two 32-key accumulators)
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[hf][r] = 0.f;
+      const uint16_t* krow = Ks + (hf * 32 + ql) * G::KSTR + 8 * hlf;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
+        sacc[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sacc[hf], 0, 0, 0);
+      }
+    }
+
+    // ---- masking
+    const int kbase = t * KT;
+    const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
+    if (need_mask) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int key = kbase + hf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hlf;
+          bool bad = key >= nk || (a.causal && key > q);
+          if (bad) sacc[hf][r] = -INFINITY;
+        }
+    }
+
+    // ---- online softmax (lane-local query; partner lane ^32 holds the other 32 keys)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f((m_run - m_new) * c);
+    const float mc = m_new * c;
+    float rs = 0.f;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = exp2f(fmaf(sacc[hf][r], c, -mc));
+        sacc[hf][r] = pv;
+        rs += pv;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < NDC; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+
+    // ---- P^T fragments (bf16), k-step kk = 2*hf + s uses regs 8s..8s+7 of sacc[hf]
+    bf16x8_t pf[4];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 u;
+        u.x = pack2(sacc[hf][8 * s + 0], sacc[hf][8 * s + 1]);
+        u.y = pack2(sacc[hf][8 * s + 2], sacc[hf][8 * s + 3]);
+        u.z = pack2(sacc[hf][8 * s + 4], sacc[hf][8 * s + 5]);
+        u.w = pack2(sacc[hf][8 * s + 6], sacc[hf][8 * s + 7]);
+        pf[2 * hf + s] = as_bf16x8(u);
+      }
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int dc = 0; dc < NDC; ++dc) {
+        const uint16_t* base = Vs + (16 * kk + tr_row) * G::VSTR + 32 * dc + tr_col;
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base));
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base + 8 * G::VSTR));
+        typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+        s16x8_t vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
+        oacc[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kk], oacc[dc], 0, 0, 0);
+      }
+    }
+
+    __syncthreads();
+    if (more) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l
+  if (q < a.Nq) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    uint16_t* Op = a.o + (long long)b * a.o_sb + (long long)q * a.o_sn + (long long)h * a.o_sh;
+#pragma unroll
+    for (int dc = 0; dc < NDC; ++dc)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        int dd = 32 * dc + 8 * g4 + 4 * hlf;
+        if (dd < d) {
+          uint2 w;
+          w.x = pack2(oacc[dc][4 * g4 + 0] * inv, oacc[dc][4 * g4 + 1] * inv);
+          w.y = pack2(oacc[dc][4 * g4 + 2] * inv, oacc[dc][4 * g4 + 3] * inv);
+          *reinterpret_cast<uint2*>(Op + dd) = w;
+        }
+      }
+  }
+}
+
+template <int DQK, int DO, int NW>
+void launch_t(const AttnArgs& a, hipStream_t s) {
+  using G = AttnGeom<DQK, DO>;
+  constexpr int QB = 32 * NW;
+  int nqb = (a.Nq + QB - 1) / QB;
+  dim3 grid(nqb * a.H * a.B);
+  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DO, NW>), grid, dim3(64 * NW), G::LDS_BYTES, s, a);
+}
+
+template <int DQK, int DO>
+void launch_nw(const AttnArgs& a, hipStream_t s) {
+  // enough workgroups to fill 256 CUs: fall back to fewer waves per block for short sequences
+  long long blocks4 = (long long)((a.Nq + 127) / 128) * a.H * a.B;
+  if (blocks4 >= 512) launch_t<DQK, DO, 4>(a, s);
+  else launch_t<DQK, DO, 2>(a, s);
+}
+
+}  // namespace
+
+void launch_attention(const AttnArgs& a, hipStream_t s) {
+  switch (a.d) {
+    case 32: launch_nw<32, 32>(a, s); break;
+    case 40: launch_nw<48, 64>(a, s); break;
+    case 64: launch_nw<64, 64>(a, s); break;
+    case 80: launch_nw<80, 96>(a, s); break;
+    case 128: launch_nw<128, 128>(a, s); break;
+    case 160: launch_nw<160, 160>(a, s); break;
+    default: {
+      // generic: round up (d must be a multiple of 8, <= 256)
+      if (a.d <= 32) launch_nw<32, 32>(a, s);
+      else if (a.d <= 64) launch_nw<64, 64>(a, s);
+      else if (a.d <= 96) launch_nw<96, 96>(a, s);
+      else if (a.d <= 128) launch_nw<128, 128>(a, s);
+      else if (a.d <= 160) launch_nw<160, 160>(a, s);
+      else launch_nw<256, 256>(a, s);
+    }
+  }
+}

@@ -1,0 +1,256 @@
+// pybind11 bindings of the gfx950 kernel library: tensor checks (fail loudly on wrong dtype,
+// device, layout or alignment), output allocation stays in Python, every launch goes to the
+// current HIP stream (so torch.cuda.graph capture records it).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+
+const uint16_t* bptr(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bptr_mut(at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* opt_bptr(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t);
+  CHECK_BF16(*t);
+  CHECK_CONTIG(*t);
+  return bptr(*t);
+}
+
+void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+          const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
+  TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
+  GemmArgs p;
+  p.A = bptr(x); p.W = bptr(w); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
+  p.M = (int)x.size(0); p.K = (int)x.size(1); p.N = (int)out.size(1); p.Nw = (int)w.size(0);
+  p.lda = (int)x.stride(0); p.ldc = p.N; p.act = (int)act;
+  TORCH_CHECK(w.size(1) == p.K, "gemm: K mismatch");
+  TORCH_CHECK(out.size(0) == p.M, "gemm: M mismatch");
+  if (act == 4) {
+    TORCH_CHECK(p.Nw == 2 * p.N && p.K % 8 == 0 && p.N % 4 == 0, "geglu: W must be [2N,K], K%8==0, N%4==0");
+  } else {
+    TORCH_CHECK(p.Nw == p.N, "gemm: N mismatch");
+  }
+  if (residual.has_value() && residual->defined()) TORCH_CHECK(residual->numel() == out.numel(), "gemm: residual shape");
+  if (out.scalar_type() == at::kFloat) {
+    p.out_f32 = 1;
+  } else {
+    CHECK_BF16(out);
+  }
+  p.C = out.data_ptr();
+  launch_gemm(p, cur_stream());
+}
+
+void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+            const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& chan_bias, at::Tensor& out,
+            int64_t stride, int64_t pad, int64_t upsample) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "conv2d: NHWC 4-D tensors expected");
+  GemmArgs p;
+  p.conv = 1;
+  p.A = bptr(x); p.W = bptr(w); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
+  p.chan_bias = opt_bptr(chan_bias);
+  p.IH = (int)x.size(1); p.IW = (int)x.size(2); p.Cin = (int)x.size(3);
+  p.ksize = (int)w.size(1);
+  TORCH_CHECK(w.size(2) == p.ksize && w.size(3) == p.Cin, "conv2d: weight must be [Cout,k,k,Cin]");
+  p.Ho = (int)out.size(1); p.Wo = (int)out.size(2);
+  p.N = (int)out.size(3); p.Nw = (int)w.size(0);
+  TORCH_CHECK(p.Nw == p.N && out.size(0) == x.size(0), "conv2d: shape mismatch");
+  p.M = (int)(x.size(0) * p.Ho * p.Wo);
+  p.K = p.ksize * p.ksize * p.Cin;
+  p.lda = p.Cin; p.ldc = p.N;
+  p.stride = (int)stride; p.pad = (int)pad; p.upsample = (int)upsample;
+  if (residual.has_value() && residual->defined()) TORCH_CHECK(residual->numel() == out.numel(), "conv2d: residual shape");
+  if (chan_bias.has_value() && chan_bias->defined())
+    TORCH_CHECK(chan_bias->numel() == x.size(0) * p.N, "conv2d: chan_bias must be [B, Cout]");
+  p.C = out.data_ptr();
+  launch_gemm(p, cur_stream());
+}
+
+// batched C[b] = alpha * A[b] @ B[b]^T ; A [Bt, M, K] (row stride free), B [Bt, N, K], C [Bt, M, N]
+void bmm_nt(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, double alpha) {
+  CHECK_DEV(a); CHECK_BF16(a); CHECK_BF16(b); CHECK_CONTIG(out);
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && out.dim() == 3, "bmm_nt: 3-D operands");
+  TORCH_CHECK(a.stride(2) == 1 && b.stride(2) == 1, "bmm_nt: K must be contiguous");
+  TORCH_CHECK(b.stride(1) == b.size(2), "bmm_nt: B rows must be packed");
+  GemmArgs p;
+  p.A = bptr(a); p.W = bptr(b);
+  p.batch = (int)a.size(0);
+  p.M = (int)a.size(1); p.K = (int)a.size(2); p.N = (int)b.size(1); p.Nw = p.N;
+  p.lda = (int)a.stride(1); p.sA = a.stride(0); p.sW = b.stride(0);
+  p.ldc = p.N; p.sC = (long long)p.M * p.N;
+  p.alpha = (float)alpha;
+  if (out.scalar_type() == at::kFloat) {
+    p.out_f32 = 1;
+  } else {
+    CHECK_BF16(out);
+  }
+  p.C = out.data_ptr();
+  launch_gemm(p, cur_stream());
+}
+
+void group_norm(const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& out,
+                int64_t groups, double eps, int64_t silu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(gamma); CHECK_BF16(beta); CHECK_CONTIG(out);
+  const int B = (int)x.size(0);
+  const int C = (int)x.size(-1);
+  const long long S = x.numel() / ((long long)B * C);
+  TORCH_CHECK(C % 8 == 0 && C % groups == 0, "group_norm: C must be a multiple of 8 and of groups");
+  auto ws = at::empty({group_norm_workspace(B, S, C)}, x.options().dtype(at::kFloat));
+  launch_group_norm(bptr(x), bptr(gamma), bptr(beta), bptr_mut(out), ws.data_ptr<float>(), B, S, C, (int)groups,
+                    (float)eps, (int)silu, cur_stream());
+}
+
+void layer_norm(const at::Tensor& x, const at::Tensor& gamma, const c10::optional<at::Tensor>& beta, at::Tensor& out,
+                double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(gamma); CHECK_CONTIG(out);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "layer_norm: D % 8 == 0 and D <= 4096");
+  launch_layer_norm(bptr(x), bptr(gamma), opt_bptr(beta), bptr_mut(out), x.numel() / D, D, (float)eps, cur_stream());
+}
+
+void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, double scale,
+               int64_t causal, const c10::optional<at::Tensor>& kv_lens, int64_t fp8) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4 && out.dim() == 4, "attention: [B,N,H,d] tensors");
+  TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1 && out.stride(3) == 1,
+              "attention: head dim must be contiguous");
+  AttnArgs a;
+  a.q = bptr(q); a.k = bptr(k); a.v = bptr(v); a.o = bptr_mut(out);
+  a.q_sb = q.stride(0); a.q_sn = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_sn = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_sn = v.stride(1); a.v_sh = v.stride(2);
+  a.o_sb = out.stride(0); a.o_sn = out.stride(1); a.o_sh = out.stride(2);
+  a.B = (int)q.size(0); a.Nq = (int)q.size(1); a.H = (int)q.size(2); a.d = (int)q.size(3);
+  a.Nk = (int)k.size(1);
+  TORCH_CHECK(a.d % 8 == 0 && a.d <= 256, "attention: head dim must be a multiple of 8 and <= 256");
+  for (long long st : {a.q_sb, a.q_sn, a.q_sh, a.k_sb, a.k_sn, a.k_sh, a.v_sb, a.v_sn, a.v_sh})
+    TORCH_CHECK(st % 8 == 0, "attention: q/k/v strides must be 16-byte aligned");
+  for (long long st : {a.o_sb, a.o_sn, a.o_sh}) TORCH_CHECK(st % 4 == 0, "attention: out strides must be 8-byte aligned");
+  a.scale = (float)scale;
+  a.causal = (int)causal;
+  a.kv_lens = nullptr;
+  if (kv_lens.has_value() && kv_lens->defined()) {
+    TORCH_CHECK(kv_lens->scalar_type() == at::kInt && kv_lens->is_cuda(), "kv_lens must be int32 on device");
+    a.kv_lens = kv_lens->data_ptr<int>();
+  }
+  (void)fp8;
+  launch_attention(a, cur_stream());
+}
+
+void gather_cosine(const at::Tensor& table, const at::Tensor& ia, const at::Tensor& ib, at::Tensor& out) {
+  CHECK_DEV(table); CHECK_CONTIG(table);
+  TORCH_CHECK(ia.scalar_type() == at::kInt && ib.scalar_type() == at::kInt, "indices must be int32");
+  int f32 = table.scalar_type() == at::kFloat;
+  if (!f32) {
+    CHECK_BF16(table);
+  }
+  launch_gather_cosine(table.data_ptr(), f32, (int)table.size(1), ia.data_ptr<int>(), ib.data_ptr<int>(),
+                       out.data_ptr<float>(), (int)ia.size(0), cur_stream());
+}
+
+void pair_cosine(const at::Tensor& a, const at::Tensor& b, at::Tensor& out) {
+  CHECK_DEV(a);
+  TORCH_CHECK(a.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "pair_cosine: f32 inputs");
+  CHECK_CONTIG(a); CHECK_CONTIG(b);
+  launch_pair_cosine(a.data_ptr<float>(), b.data_ptr<float>(), (int)a.size(1), out.data_ptr<float>(), (int)a.size(0),
+                     cur_stream());
+}
+
+void cosine_gemv(const at::Tensor& table, const at::Tensor& vec, at::Tensor& out) {
+  CHECK_DEV(table); CHECK_CONTIG(table); CHECK_CONTIG(vec);
+  int tf = table.scalar_type() == at::kFloat, vf = vec.scalar_type() == at::kFloat;
+  launch_cosine_gemv(table.data_ptr(), tf, (int)table.size(0), (int)table.size(1), vec.data_ptr(), vf,
+                     out.data_ptr<float>(), cur_stream());
+}
+
+void mean_pool_l2(const at::Tensor& h, const at::Tensor& lens, at::Tensor& out) {
+  CHECK_DEV(h); CHECK_BF16(h); CHECK_CONTIG(h);
+  TORCH_CHECK(lens.scalar_type() == at::kInt, "lens must be int32");
+  launch_mean_pool_l2(bptr(h), lens.data_ptr<int>(), out.data_ptr<float>(), (int)h.size(0), (int)h.size(1),
+                      (int)h.size(2), cur_stream());
+}
+
+void gaussian_blur(const at::Tensor& img, const at::Tensor& w, at::Tensor& out) {
+  CHECK_DEV(img); CHECK_CONTIG(img);
+  TORCH_CHECK(img.dim() == 3, "gaussian_blur: [H, W, C]");
+  int u8 = img.scalar_type() == at::kByte;
+  if (!u8) {
+    TORCH_CHECK(img.scalar_type() == at::kFloat, "gaussian_blur: uint8 or f32");
+  }
+  auto wf = w.to(at::kFloat).contiguous();
+  int R = (int)(wf.numel() - 1) / 2;
+  auto tmp = at::empty({img.numel()}, img.options().dtype(at::kFloat));
+  launch_gaussian_blur(img.data_ptr(), u8, (int)img.size(0), (int)img.size(1), (int)img.size(2), wf.data_ptr<float>(),
+                       R, tmp.data_ptr<float>(), out.data_ptr(), cur_stream());
+}
+
+void to_uint8(const at::Tensor& x, at::Tensor& out) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  launch_to_uint8(bptr(x), out.data_ptr<uint8_t>(), x.numel(), cur_stream());
+}
+
+void timestep_embedding(const at::Tensor& t, at::Tensor& out, int64_t flip, double shift) {
+  CHECK_DEV(t);
+  launch_timestep_embedding(t.data_ptr<float>(), out.data_ptr<float>(), (int)t.size(0), (int)out.size(1), (int)flip,
+                            (float)shift, cur_stream());
+}
+
+void latent_step(const at::Tensor& eps, at::Tensor& x, at::Tensor& hist, at::Tensor& xs, const at::Tensor& coef,
+                 const at::Tensor& step, at::Tensor& unet_in, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(eps); CHECK_CONTIG(eps); CHECK_BF16(unet_in);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && hist.scalar_type() == at::kFloat && xs.scalar_type() == at::kFloat,
+              "latent_step: f32 master latents");
+  TORCH_CHECK(step.scalar_type() == at::kInt, "latent_step: int32 step counter");
+  const long long n = x.numel();
+  TORCH_CHECK(eps.numel() == (cfg ? 2 * n : n) && unet_in.numel() == eps.numel() && hist.numel() == 4 * n,
+              "latent_step: shape mismatch");
+  launch_latent_step(bptr(eps), x.data_ptr<float>(), hist.data_ptr<float>(), xs.data_ptr<float>(),
+                     coef.data_ptr<float>(), step.data_ptr<int>(), bptr_mut(unet_in), n, (int)cfg, cur_stream());
+}
+
+void advance_step(at::Tensor& step) { launch_advance_step(step.data_ptr<int>(), cur_stream()); }
+
+void softmax_rows(const at::Tensor& S, at::Tensor& P, int64_t causal, const c10::optional<at::Tensor>& kv_lens) {
+  CHECK_DEV(S); CHECK_CONTIG(S); CHECK_CONTIG(P);
+  TORCH_CHECK(S.scalar_type() == at::kFloat, "softmax_rows: f32 scores");
+  const int cols = (int)S.size(-1);
+  const int Nq = (int)S.size(-2);
+  const int rows = (int)(S.numel() / cols);
+  const int* kl = nullptr;
+  if (kv_lens.has_value() && kv_lens->defined()) kl = kv_lens->data_ptr<int>();
+  launch_softmax_rows(S.data_ptr<float>(), bptr_mut(P), rows, cols, Nq, (int)causal, kl, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
+  m.def("gemm", &gemm);
+  m.def("conv2d", &conv2d);
+  m.def("bmm_nt", &bmm_nt);
+  m.def("group_norm", &group_norm);
+  m.def("layer_norm", &layer_norm);
+  m.def("attention", &attention);
+  m.def("gather_cosine", &gather_cosine);
+  m.def("pair_cosine", &pair_cosine);
+  m.def("cosine_gemv", &cosine_gemv);
+  m.def("mean_pool_l2", &mean_pool_l2);
+  m.def("gaussian_blur", &gaussian_blur);
+  m.def("to_uint8", &to_uint8);
+  m.def("timestep_embedding", &timestep_embedding);
+  m.def("latent_step", &latent_step);
+  m.def("advance_step", &advance_step);
+  m.def("softmax_rows", &softmax_rows);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,85 @@
+// Shared device helpers for the cassmantle_amd gfx950 (CDNA4) kernel library.
+//
+// Conventions: bf16 tensors are handled as raw 16-bit words (uint16_t) and moved 16 bytes per
+// lane (8 x bf16, `uint4`), never element by element (cdna_hip_programming.md G13).  MFMA
+// operands use the gfx950 bf16 vector types; accumulators are f32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+#define CM_DEVICE __device__ __forceinline__
+
+CM_DEVICE float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN preserved: quiet bit forced)
+CM_DEVICE uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+CM_DEVICE uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+CM_DEVICE void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+CM_DEVICE uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+CM_DEVICE bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+CM_DEVICE float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+CM_DEVICE float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+CM_DEVICE float gelu_tanh_f(float x) {
+  const float k = 0.7978845608028654f;
+  return 0.5f * x * (1.0f + tanhf(k * (x + 0.044715f * x * x * x)));
+}
+CM_DEVICE float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+
+// activation codes shared with python (ops/__init__.py _ACT)
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_QUICK_GELU = 3, ACT_GEGLU = 4, ACT_GELU_TANH = 5 };
+
+CM_DEVICE float apply_act(float x, int act) {
+  switch (act) {
+    case ACT_GELU: return gelu_f(x);
+    case ACT_SILU: return silu_f(x);
+    case ACT_QUICK_GELU: return quick_gelu_f(x);
+    case ACT_GELU_TANH: return gelu_tanh_f(x);
+    default: return x;
+  }
+}
+
+CM_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+CM_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5 / T1):
+// consecutive logical tiles land on the same XCD (shared L2) under round-robin dispatch.
+CM_DEVICE int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  int q = nblocks / nx, r = nblocks % nx;
+  int xcd = bid % nx, idx = bid / nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

@@ -1,0 +1,63 @@
+// Host-visible launcher declarations of the gfx950 kernel library.  Kernel translation units
+// (*.hip) are compiled without torch headers; bindings.cpp converts tensors to these structs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct GemmArgs {
+  const uint16_t* A = nullptr;          // activations [batch][M][lda] or NHWC conv input
+  const uint16_t* W = nullptr;          // weights [batch][Nw][K], K contiguous
+  const uint16_t* bias = nullptr;       // [Nw] (geglu: [2N])
+  const uint16_t* residual = nullptr;   // [M][ldc]
+  const uint16_t* chan_bias = nullptr;  // [B][N] per-image bias (ResNet time embedding)
+  void* C = nullptr;                    // [batch][M][ldc] bf16 or f32
+  int M = 0, N = 0, K = 0, Nw = 0;
+  int lda = 0, ldc = 0;
+  long long sA = 0, sW = 0, sC = 0;
+  int batch = 1;
+  float alpha = 1.f;
+  int act = 0;
+  int out_f32 = 0;
+  // implicit-GEMM convolution (conv != 0)
+  int conv = 0, IH = 0, IW = 0, Cin = 0, Ho = 0, Wo = 0, stride = 1, pad = 0, ksize = 1, upsample = 0;
+};
+void launch_gemm(const GemmArgs& p, hipStream_t s);
+
+struct AttnArgs {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o;
+  long long q_sb, q_sn, q_sh;     // element strides: batch, token, head
+  long long k_sb, k_sn, k_sh;
+  long long v_sb, v_sn, v_sh;
+  long long o_sb, o_sn, o_sh;
+  int B, H, Nq, Nk, d;
+  float scale;
+  int causal;
+  const int* kv_lens;             // [B] or null
+};
+void launch_attention(const AttnArgs& a, hipStream_t s);
+
+// norms
+void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                       float* ws, int B, long long S, int C, int G, float eps, int silu, hipStream_t s);
+long long group_norm_workspace(int B, long long S, int C);
+void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                       long long rows, int D, float eps, hipStream_t s);
+
+// scorer
+void launch_gather_cosine(const void* table, int table_f32, int D, const int* ia, const int* ib,
+                          float* out, int n, hipStream_t s);
+void launch_pair_cosine(const float* a, const float* b, int D, float* out, int n, hipStream_t s);
+void launch_cosine_gemv(const void* table, int table_f32, int V, int D, const void* vec, int vec_f32,
+                        float* out, hipStream_t s);
+void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, int T, int D, hipStream_t s);
+
+// image / diffusion glue
+void launch_gaussian_blur(const void* img, int u8, int H, int W, int C, const float* w, int R,
+                          float* tmp, void* out, hipStream_t s);
+void launch_to_uint8(const uint16_t* x, uint8_t* out, long long n, hipStream_t s);
+void launch_timestep_embedding(const float* t, float* out, int B, int dim, int flip, float shift, hipStream_t s);
+void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef,
+                        const int* step, uint16_t* unet_in, long long n, int cfg, hipStream_t s);
+void launch_advance_step(int* step, hipStream_t s);
+void launch_softmax_rows(const float* S, uint16_t* P, int rows, int cols, int Nq, int causal,
+                         const int* kv_lens, hipStream_t s);

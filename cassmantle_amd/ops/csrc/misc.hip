@@ -1,0 +1,284 @@
+// Scorer, image and diffusion-glue kernels.
+//
+// * gather_cosine (K14): one wave per (guess, answer) pair: gather both table rows (bf16 or
+//   f32), dot and both norms in one pass, wave reduction; OOV (-1) -> NaN.  A whole
+//   micro-batch of players' guesses is one launch.
+// * pair_cosine: row-wise cosine of two embedding matrices (MiniLM scorer).
+// * cosine_gemv (K15): table . v / (|row| |v|) for most_similar, one wave per row.
+// * mean_pool_l2 (K16 tail): masked mean over tokens + L2 normalisation, one block per row.
+// * gaussian_blur (K17): separable blur, horizontal pass -> f32 scratch -> vertical pass,
+//   edge clamp, uint8 or f32 images.
+// * to_uint8 (K18): VAE output [-1, 1] -> uint8 (x/2 + 0.5 clamp, *255, round).
+// * timestep_embedding (K10), latent_step (K11: CFG combine + scheduler update + next UNet
+//   input, reading its coefficient row through a device step counter so a hipGraph replays
+//   it unchanged), advance_step, softmax_rows (VAE d=512 attention path).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+template <bool F32>
+CM_DEVICE float ld(const void* p, long long i) {
+  if constexpr (F32) return reinterpret_cast<const float*>(p)[i];
+  else return bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+}
+
+template <bool F32>
+__global__ void gather_cosine_kernel(const void* __restrict__ table, int D, const int* __restrict__ ia,
+                                     const int* __restrict__ ib, float* __restrict__ out, int n) {
+  const int lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (pair >= n) return;
+  const int a = ia[pair], b = ib[pair];
+  if (a < 0 || b < 0) {
+    if (lane == 0) out[pair] = __builtin_nanf("");
+    return;
+  }
+  float dot = 0.f, na = 0.f, nb = 0.f;
+  for (int k = lane; k < D; k += 64) {
+    float x = ld<F32>(table, (long long)a * D + k), y = ld<F32>(table, (long long)b * D + k);
+    dot = fmaf(x, y, dot); na = fmaf(x, x, na); nb = fmaf(y, y, nb);
+  }
+  dot = wave_sum(dot); na = wave_sum(na); nb = wave_sum(nb);
+  if (lane == 0) out[pair] = dot / fmaxf(sqrtf(na) * sqrtf(nb), 1e-12f);
+}
+
+__global__ void pair_cosine_kernel(const float* __restrict__ A, const float* __restrict__ Bm, int D,
+                                   float* __restrict__ out, int n) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float dot = 0.f, na = 0.f, nb = 0.f;
+  for (int k = lane; k < D; k += 64) {
+    float x = A[(long long)row * D + k], y = Bm[(long long)row * D + k];
+    dot = fmaf(x, y, dot); na = fmaf(x, x, na); nb = fmaf(y, y, nb);
+  }
+  dot = wave_sum(dot); na = wave_sum(na); nb = wave_sum(nb);
+  if (lane == 0) out[row] = dot / fmaxf(sqrtf(na) * sqrtf(nb), 1e-12f);
+}
+
+template <bool TF32, bool VF32>
+__global__ void cosine_gemv_kernel(const void* __restrict__ table, int V, int D, const void* __restrict__ vec,
+                                   float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= V) return;
+  float dot = 0.f, nt = 0.f, nv = 0.f;
+  for (int k = lane; k < D; k += 64) {
+    float x = ld<TF32>(table, (long long)row * D + k), y = ld<VF32>(vec, k);
+    dot = fmaf(x, y, dot); nt = fmaf(x, x, nt); nv = fmaf(y, y, nv);
+  }
+  dot = wave_sum(dot); nt = wave_sum(nt); nv = wave_sum(nv);
+  if (lane == 0) out[row] = dot / fmaxf(sqrtf(nt) * sqrtf(nv), 1e-12f);
+}
+
+__global__ void mean_pool_l2_kernel(const uint16_t* __restrict__ h, const int* __restrict__ lens,
+                                    float* __restrict__ out, int T, int D) {
+  extern __shared__ float buf[];   // [D] + [64]
+  const int b = blockIdx.x;
+  const int L = max(1, min(T, lens[b]));
+  float* red = buf + D;
+  float ss = 0.f;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < L; ++t) s += bf2f(h[((long long)b * T + t) * D + d]);
+    s /= (float)L;
+    buf[d] = s;
+    ss = fmaf(s, s, ss);
+  }
+  ss = wave_sum(ss);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) red[w] = ss;
+  __syncthreads();
+  float tot = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
+  const float inv = 1.f / fmaxf(sqrtf(tot), 1e-12f);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) out[(long long)b * D + d] = buf[d] * inv;
+}
+
+template <bool U8>
+__global__ void blur_h_kernel(const void* __restrict__ img, int H, int W, int C, const float* __restrict__ w,
+                              int R, float* __restrict__ tmp) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long n = (long long)H * W * C;
+  if (i >= n) return;
+  int c = (int)(i % C);
+  long long px = i / C;
+  int x = (int)(px % W), y = (int)(px / W);
+  float s = 0.f;
+  for (int k = -R; k <= R; ++k) {
+    int xx = min(max(x + k, 0), W - 1);
+    long long j = ((long long)y * W + xx) * C + c;
+    float v = U8 ? (float)reinterpret_cast<const uint8_t*>(img)[j] : reinterpret_cast<const float*>(img)[j];
+    s = fmaf(w[k + R], v, s);
+  }
+  tmp[i] = s;
+}
+
+template <bool U8>
+__global__ void blur_v_kernel(const float* __restrict__ tmp, int H, int W, int C, const float* __restrict__ w,
+                              int R, void* __restrict__ out) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long n = (long long)H * W * C;
+  if (i >= n) return;
+  int c = (int)(i % C);
+  long long px = i / C;
+  int x = (int)(px % W), y = (int)(px / W);
+  float s = 0.f;
+  for (int k = -R; k <= R; ++k) {
+    int yy = min(max(y + k, 0), H - 1);
+    s = fmaf(w[k + R], tmp[((long long)yy * W + x) * C + c], s);
+  }
+  if (U8) reinterpret_cast<uint8_t*>(out)[i] = (uint8_t)fminf(fmaxf(rintf(s), 0.f), 255.f);
+  else reinterpret_cast<float*>(out)[i] = s;
+}
+
+__global__ void to_uint8_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ out, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = bf2f(x[i]) * 0.5f + 0.5f;
+  v = fminf(fmaxf(v, 0.f), 1.f) * 255.f;
+  out[i] = (uint8_t)rintf(v);
+}
+
+__global__ void timestep_embedding_kernel(const float* __restrict__ t, float* __restrict__ out, int B, int dim,
+                                          int flip, float shift) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int half = dim / 2;
+  if (i >= B * half) return;
+  int b = i / half, k = i % half;
+  float ex = -logf(10000.f) * (float)k / ((float)half - shift);
+  float arg = t[b] * expf(ex);
+  float sv = sinf(arg), cv = cosf(arg);
+  if (flip) { out[b * dim + k] = cv; out[b * dim + half + k] = sv; }
+  else { out[b * dim + k] = sv; out[b * dim + half + k] = cv; }
+}
+
+// coefficient row layout: see models/schedulers.py
+__global__ void latent_step_kernel(const uint16_t* __restrict__ eps, float* __restrict__ x,
+                                   float* __restrict__ hist, float* __restrict__ xs,
+                                   const float* __restrict__ coef, const int* __restrict__ step,
+                                   uint16_t* __restrict__ unet_in, long long n, int cfg) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* r = coef + 16 * step[0];
+  float e;
+  if (cfg) {
+    float u = bf2f(eps[i]), c = bf2f(eps[n + i]);
+    e = u + r[13] * (c - u);
+  } else {
+    e = bf2f(eps[i]);
+  }
+  float ep = r[0] * e;
+  int s1 = (int)r[8], s2 = (int)r[9], s3 = (int)r[10], sv = (int)r[11];
+  if (s1 >= 0) ep = fmaf(r[1], hist[(long long)s1 * n + i], ep);
+  if (s2 >= 0) ep = fmaf(r[2], hist[(long long)s2 * n + i], ep);
+  if (s3 >= 0) ep = fmaf(r[3], hist[(long long)s3 * n + i], ep);
+  float xo = x[i];
+  float xn = r[4] * xo + r[5] * xs[i] + r[6] * ep;
+  if (sv >= 0) hist[(long long)sv * n + i] = e;
+  if (r[12] > 0.f) xs[i] = xo;
+  x[i] = xn;
+  uint16_t o = f2bf(r[7] * xn);
+  unet_in[i] = o;
+  if (cfg) unet_in[n + i] = o;
+}
+
+__global__ void advance_step_kernel(int* step) { step[0] += 1; }
+
+// row softmax with optional causal / key-length mask (S fp32 [rows][cols] -> P bf16)
+__global__ void softmax_rows_kernel(const float* __restrict__ S, uint16_t* __restrict__ P, int cols, int Nq,
+                                    int causal, const int* __restrict__ kv_lens) {
+  __shared__ float red[16];
+  const long long row = blockIdx.x;
+  const int qi = (int)(row % Nq);
+  const int b = (int)(row / Nq);
+  int lim = cols;
+  if (kv_lens) lim = min(lim, kv_lens[b]);
+  if (causal) lim = min(lim, qi + 1);
+  const float* s = S + row * cols;
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < lim; j += blockDim.x) mx = fmaxf(mx, s[j]);
+  mx = wave_max(mx);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = -INFINITY;
+  for (int i = 0; i < nw; ++i) mx = fmaxf(mx, red[i]);
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = threadIdx.x; j < lim; j += blockDim.x) sum += __expf(s[j] - mx);
+  sum = wave_sum(sum);
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  sum = 0.f;
+  for (int i = 0; i < nw; ++i) sum += red[i];
+  const float inv = 1.f / sum;
+  for (int j = threadIdx.x; j < cols; j += blockDim.x)
+    P[row * cols + j] = f2bf(j < lim ? __expf(s[j] - mx) * inv : 0.f);
+}
+
+inline unsigned nblk(long long n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+void launch_gather_cosine(const void* table, int table_f32, int D, const int* ia, const int* ib, float* out,
+                          int n, hipStream_t s) {
+  if (n <= 0) return;
+  if (table_f32) hipLaunchKernelGGL(gather_cosine_kernel<true>, dim3(nblk(n, 4)), dim3(256), 0, s, table, D, ia, ib, out, n);
+  else hipLaunchKernelGGL(gather_cosine_kernel<false>, dim3(nblk(n, 4)), dim3(256), 0, s, table, D, ia, ib, out, n);
+}
+
+void launch_pair_cosine(const float* a, const float* b, int D, float* out, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pair_cosine_kernel, dim3(nblk(n, 4)), dim3(256), 0, s, a, b, D, out, n);
+}
+
+void launch_cosine_gemv(const void* table, int table_f32, int V, int D, const void* vec, int vec_f32, float* out,
+                        hipStream_t s) {
+  dim3 g(nblk(V, 4));
+  if (table_f32 && vec_f32) hipLaunchKernelGGL((cosine_gemv_kernel<true, true>), g, dim3(256), 0, s, table, V, D, vec, out);
+  else if (table_f32) hipLaunchKernelGGL((cosine_gemv_kernel<true, false>), g, dim3(256), 0, s, table, V, D, vec, out);
+  else if (vec_f32) hipLaunchKernelGGL((cosine_gemv_kernel<false, true>), g, dim3(256), 0, s, table, V, D, vec, out);
+  else hipLaunchKernelGGL((cosine_gemv_kernel<false, false>), g, dim3(256), 0, s, table, V, D, vec, out);
+}
+
+void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, int T, int D, hipStream_t s) {
+  hipLaunchKernelGGL(mean_pool_l2_kernel, dim3(B), dim3(256), (D + 64) * sizeof(float), s, h, lens, out, T, D);
+}
+
+void launch_gaussian_blur(const void* img, int u8, int H, int W, int C, const float* w, int R, float* tmp,
+                          void* out, hipStream_t s) {
+  long long n = (long long)H * W * C;
+  if (u8) {
+    hipLaunchKernelGGL(blur_h_kernel<true>, dim3(nblk(n, 256)), dim3(256), 0, s, img, H, W, C, w, R, tmp);
+    hipLaunchKernelGGL(blur_v_kernel<true>, dim3(nblk(n, 256)), dim3(256), 0, s, tmp, H, W, C, w, R, out);
+  } else {
+    hipLaunchKernelGGL(blur_h_kernel<false>, dim3(nblk(n, 256)), dim3(256), 0, s, img, H, W, C, w, R, tmp);
+    hipLaunchKernelGGL(blur_v_kernel<false>, dim3(nblk(n, 256)), dim3(256), 0, s, tmp, H, W, C, w, R, out);
+  }
+}
+
+void launch_to_uint8(const uint16_t* x, uint8_t* out, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(to_uint8_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, x, out, n);
+}
+
+void launch_timestep_embedding(const float* t, float* out, int B, int dim, int flip, float shift, hipStream_t s) {
+  hipLaunchKernelGGL(timestep_embedding_kernel, dim3(nblk((long long)B * dim / 2, 256)), dim3(256), 0, s, t, out, B,
+                     dim, flip, shift);
+}
+
+void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef, const int* step,
+                        uint16_t* unet_in, long long n, int cfg, hipStream_t s) {
+  hipLaunchKernelGGL(latent_step_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, eps, x, hist, xs, coef, step, unet_in,
+                     n, cfg);
+}
+
+void launch_advance_step(int* step, hipStream_t s) {
+  hipLaunchKernelGGL(advance_step_kernel, dim3(1), dim3(1), 0, s, step);
+}
+
+void launch_softmax_rows(const float* S, uint16_t* P, int rows, int cols, int Nq, int causal, const int* kv_lens,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(rows), dim3(256), 0, s, S, P, cols, Nq, causal, kv_lens);
+}

@@ -1,0 +1,237 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the same op
+(``cassmantle_amd.ops.reference``), on the GPU.  Inputs are asymmetric random data so a
+transposed MFMA layout or swapped index cannot pass (cdna_hip_programming.md §3)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from cassmantle_amd import ops  # noqa: E402
+from cassmantle_amd.ops import reference as ref  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _ext_loaded():
+    from cassmantle_amd.ops._ext import ext_available, ext_error
+    assert ext_available(), ext_error()
+    ops.set_mode("hip")
+
+
+@pytest.mark.parametrize("M,N,K", [(257, 320, 320), (100, 64, 96), (4096, 640, 1280), (77, 768, 768), (5, 1280, 320)])
+@pytest.mark.parametrize("act", [None, "gelu", "silu", "quick_gelu"])
+def test_gemm(M, N, K, act):
+    x = rnd(M, K, seed=1)
+    w = rnd(N, K, scale=K ** -0.5, seed=2)
+    b = rnd(N, scale=0.1, seed=3)
+    r = rnd(M, N, seed=4)
+    out = ops.linear(x, w, b, residual=r, act=act)
+    exp = ref.linear(x, w, b, residual=r, act=act)
+    assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 320, 320), (4096, 1280, 320), (33, 64, 64)])
+def test_gemm_geglu(M, N, K):
+    x = rnd(M, K, seed=5)
+    w = rnd(2 * N, K, scale=K ** -0.5, seed=6)
+    b = rnd(2 * N, scale=0.1, seed=7)
+    out = ops.linear(x, w, b, act="geglu")
+    exp = ref.linear(x, w, b, act="geglu")
+    assert rel_err(out, exp) < 1e-2
+
+
+def test_gemm_small_k():
+    # K % 8 != 0 -> SIMT path (post_quant_conv 4->4)
+    x = rnd(1000, 4, seed=8)
+    w = rnd(4, 4, seed=9)
+    assert rel_err(ops.linear(x, w), ref.linear(x, w)) < 1e-2
+
+
+def test_bmm_nt_f32():
+    from cassmantle_amd.ops._ext import ext
+    a = rnd(2, 300, 512, seed=10)
+    b = rnd(2, 200, 512, seed=11)
+    out = torch.empty(2, 300, 200, device=DEV, dtype=torch.float32)
+    ext().bmm_nt(a, b, out, 0.5)
+    exp = 0.5 * torch.matmul(a.float(), b.float().transpose(1, 2))
+    assert rel_err(out, exp) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,stride,up", [
+    (2, 17, 13, 64, 128, 1, False),
+    (2, 16, 16, 320, 320, 2, False),
+    (1, 8, 8, 128, 64, 1, True),
+    (2, 9, 11, 32, 64, 1, False),     # Cin % 64 != 0 general path
+    (1, 12, 12, 4, 64, 1, False),     # conv_in (SIMT)
+    (1, 12, 12, 128, 3, 1, False),    # VAE conv_out (SIMT)
+])
+def test_conv(B, H, W, Cin, Cout, stride, up):
+    x = rnd(B, H, W, Cin, seed=12)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=13)
+    b = rnd(Cout, scale=0.1, seed=14)
+    out = ops.conv2d(x, w, b, stride=stride, padding=1, upsample=up)
+    exp = ref.conv2d(x, w, b, stride=stride, padding=1, upsample=up)
+    assert out.shape == exp.shape
+    assert rel_err(out, exp) < 1e-2
+
+
+def test_conv_epilogue_fusions():
+    B, H, W, C = 2, 16, 16, 64
+    x = rnd(B, H, W, C, seed=15)
+    w = rnd(C, 3, 3, C, scale=(9 * C) ** -0.5, seed=16)
+    cb = rnd(B, C, seed=17)
+    res = rnd(B, H, W, C, seed=18)
+    out = ops.conv2d(x, w, None, residual=res, chan_bias=cb)
+    exp = ref.conv2d(x, w, None, residual=res, chan_bias=cb)
+    assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("shape,G,silu,eps", [
+    ((2, 8, 8, 320), 32, True, 1e-5),
+    ((1, 64, 64, 128), 32, False, 1e-6),
+    ((2, 8, 8, 2560), 32, True, 1e-5),
+    ((3, 5, 7, 64), 8, True, 1e-5),
+    ((2, 4096, 320), 32, False, 1e-6),
+])
+def test_group_norm(shape, G, silu, eps):
+    x = rnd(*shape, seed=19) + 0.5
+    C = shape[-1]
+    g = rnd(C, seed=20) * 0.5 + 1
+    b = rnd(C, seed=21) * 0.1
+    out = ops.group_norm(x, G, g, b, eps, silu)
+    exp = ref.group_norm(x, G, g, b, eps, silu)
+    assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("D", [320, 384, 768, 1280, 32])
+def test_layer_norm(D):
+    x = rnd(333, D, seed=22) * 2 + 1
+    g = rnd(D, seed=23) * 0.5 + 1
+    b = rnd(D, seed=24) * 0.1
+    assert rel_err(ops.layer_norm(x, g, b, 1e-5), ref.layer_norm(x, g, b, 1e-5)) < 1e-2
+
+
+@pytest.mark.parametrize("B,Nq,Nk,H,d,causal", [
+    (2, 300, 300, 8, 40, False),
+    (2, 1024, 77, 8, 80, False),
+    (2, 256, 256, 8, 160, False),
+    (2, 77, 77, 12, 64, True),
+    (3, 16, 16, 12, 32, False),
+    (1, 64, 64, 8, 160, False),
+    (1, 4096, 4096, 8, 40, False),
+])
+def test_attention(B, Nq, Nk, H, d, causal):
+    q = rnd(B, Nq, H, d, seed=25)
+    k = rnd(B, Nk, H, d, seed=26)
+    v = rnd(B, Nk, H, d, seed=27)
+    out = ops.attention(q, k, v, causal=causal)
+    exp = ref.attention(q, k, v, causal=causal)
+    assert rel_err(out, exp) < 2e-2
+
+
+def test_attention_strided_qkv_and_kv_lens():
+    B, N, H, d = 3, 20, 12, 32
+    qkv = rnd(B, N, 3, H, d, seed=28)
+    lens = torch.tensor([20, 7, 13], dtype=torch.int32, device=DEV)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    out = ops.attention(q, k, v, kv_lens=lens)
+    exp = ref.attention(q, k, v, kv_lens=lens)
+    assert rel_err(out, exp) < 2e-2
+
+
+def test_attention_large_head_dim_gemm_path():
+    B, N, d = 1, 1024, 512
+    qkv = rnd(B, N, 3, 1, d, seed=29)
+    out = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
+    exp = ref.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
+    assert rel_err(out, exp) < 2e-2
+
+
+def test_attention_softmax_spike():
+    # force the online-softmax rescale: one key dominates late in the sequence
+    B, N, H, d = 1, 512, 2, 64
+    q = rnd(B, N, H, d, seed=30)
+    k = rnd(B, N, H, d, seed=31)
+    k[:, 400] = q[:, 5] * 4
+    v = rnd(B, N, H, d, seed=32)
+    assert rel_err(ops.attention(q, k, v), ref.attention(q, k, v)) < 2e-2
+
+
+def test_scorer_kernels():
+    t = rnd(1000, 300, dtype=torch.float32, seed=33)
+    ia = torch.tensor([0, 5, -1, 999], dtype=torch.int32, device=DEV)
+    ib = torch.tensor([1, 5, 3, 0], dtype=torch.int32, device=DEV)
+    out = ops.gather_cosine(t, ia, ib)
+    exp = ref.gather_cosine(t, ia, ib)
+    assert torch.isnan(out[2]) and torch.isnan(exp[2])
+    m = ~torch.isnan(exp)
+    assert torch.allclose(out[m], exp[m], atol=1e-5)
+    tb = t.to(torch.bfloat16)
+    out = ops.gather_cosine(tb, ia, ib)
+    exp = ref.gather_cosine(tb, ia, ib)
+    assert torch.allclose(out[m], exp[m], atol=1e-3)
+    a, b = rnd(64, 384, dtype=torch.float32, seed=34), rnd(64, 384, dtype=torch.float32, seed=35)
+    assert torch.allclose(ops.pair_cosine(a, b), ref.pair_cosine(a, b), atol=1e-5)
+    v, i = ops.cosine_topk(t, t[7], 5)
+    ve, ie = ref.cosine_topk(t, t[7], 5)
+    assert i[0].item() == 7 and torch.equal(i, ie)
+    h = rnd(4, 16, 384, seed=36)
+    lens = torch.tensor([16, 3, 9, 1], dtype=torch.int32, device=DEV)
+    assert torch.allclose(ops.mean_pool_l2(h, lens), ref.mean_pool_l2(h, lens), atol=1e-4)
+
+
+def test_image_kernels():
+    img = (torch.rand(64, 48, 3, generator=torch.Generator().manual_seed(37)) * 255).to(torch.uint8).to(DEV)
+    out = ops.gaussian_blur(img, 3.0)
+    exp = ref.gaussian_blur(img, 3.0)
+    assert (out.int() - exp.int()).abs().max().item() <= 1
+    x = rnd(2, 16, 16, 3, seed=38) * 1.5
+    u = ops.vae_postprocess(x)
+    ue = ((x.float() / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+    assert (u.int() - ue.int()).abs().max().item() <= 1
+
+
+def test_timestep_embedding():
+    t = torch.tensor([981.0, 1.0, 500.0], device=DEV)
+    assert torch.allclose(ops.timestep_embedding(t, 320), ref.timestep_embedding(t, 320), atol=2e-3)
+
+
+@pytest.mark.parametrize("sched", ["pndm", "ddim", "euler"])
+def test_latent_step_matches_reference(sched):
+    from cassmantle_amd.models.schedulers import latent_step_reference, make_plan
+    plan = make_plan(sched, 10, 7.5)
+    B, n = 2, 8 * 8 * 4
+    g = torch.Generator().manual_seed(39)
+    x0 = torch.randn(B, 8, 8, 4, generator=g)
+    state = []
+    for dev in ("cpu", DEV):
+        x = x0.clone().to(dev)
+        hist = torch.zeros(4, B, 8, 8, 4, device=dev)
+        xs = torch.zeros_like(x)
+        unet_in = torch.zeros(2 * B, 8, 8, 4, device=dev, dtype=torch.bfloat16)
+        coef = torch.from_numpy(plan.table).to(dev)
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        for i in range(plan.evals):
+            eps = torch.randn(2 * B, 8, 8, 4, generator=torch.Generator().manual_seed(100 + i)).to(torch.bfloat16).to(dev)
+            if dev == "cpu":
+                latent_step_reference(eps, x, hist, xs, coef, step, unet_in, True)
+                step += 1
+            else:
+                ops.latent_step(eps, x, hist, xs, coef, step, unet_in, True)
+                ops.advance_step(step)
+        state.append(x.cpu())
+    assert rel_err(state[1], state[0]) < 1e-4
