@@ -82,12 +82,11 @@ void bmm_nt(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, double al
   CHECK_DEV(a); CHECK_BF16(a); CHECK_BF16(b); CHECK_CONTIG(out);
   TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && out.dim() == 3, "bmm_nt: 3-D operands");
   TORCH_CHECK(a.stride(2) == 1 && b.stride(2) == 1, "bmm_nt: K must be contiguous");
-  TORCH_CHECK(b.stride(1) == b.size(2), "bmm_nt: B rows must be packed");
   GemmArgs p;
   p.A = bptr(a); p.W = bptr(b);
   p.batch = (int)a.size(0);
   p.M = (int)a.size(1); p.K = (int)a.size(2); p.N = (int)b.size(1); p.Nw = p.N;
-  p.lda = (int)a.stride(1); p.sA = a.stride(0); p.sW = b.stride(0);
+  p.lda = (int)a.stride(1); p.ldw = (int)b.stride(1); p.sA = a.stride(0); p.sW = b.stride(0);
   p.ldc = p.N; p.sC = (long long)p.M * p.N;
   p.alpha = (float)alpha;
   if (out.scalar_type() == at::kFloat) {

@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
 
   const uint16_t* __restrict__ A = p.A + (long long)batch * p.sA;
   const uint16_t* __restrict__ W = p.W + (long long)batch * p.sW;
+  const int ldw = p.ldw ? p.ldw : p.K;
 
   // ---- per-thread load assignment: chunk c, rows r0 + 32*i
   constexpr int AR = BM / 32, WR = BN / 32;
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (wrow_[i] >= 0 && k < p.K) v = *reinterpret_cast<const uint4*>(W + (long long)wrow_[i] * p.K + k);
+      if (wrow_[i] >= 0 && k < p.K) v = *reinterpret_cast<const uint4*>(W + (long long)wrow_[i] * ldw + k);
       rw[i] = v;
     }
   };
@@ -268,7 +269,7 @@ __global__ void gemm_simt_kernel(GemmArgs p) {
   int m = (int)(idx / p.N), n = (int)(idx - (long long)m * p.N);
   const int batch = blockIdx.z;
   const uint16_t* A = p.A + (long long)batch * p.sA;
-  const uint16_t* W = p.W + (long long)batch * p.sW + (long long)n * p.K;
+  const uint16_t* W = p.W + (long long)batch * p.sW + (long long)n * (p.ldw ? p.ldw : p.K);
   float s = 0.f;
   if constexpr (CONV == 0) {
     const uint16_t* a = A + (long long)m * p.lda;
@@ -326,7 +327,8 @@ void launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 void launch_gemm(const GemmArgs& p, hipStream_t s) {
   const bool mfma_ok = (p.K % 8 == 0) && (p.N % 4 == 0) && (p.ldc % 4 == 0) &&
-                       (!p.conv || p.Cin % 8 == 0) && (p.conv || p.lda % 8 == 0);
+                       (!p.conv || p.Cin % 8 == 0) && (p.conv || p.lda % 8 == 0) &&
+                       (p.ldw % 8 == 0);
   if (!mfma_ok) {
     if (p.act == ACT_GEGLU) return;  // host side guarantees geglu shapes are MFMA-able
     long long total = (long long)p.M * p.N;

@@ -12,7 +12,7 @@ struct GemmArgs {
   const uint16_t* chan_bias = nullptr;  // [B][N] per-image bias (ResNet time embedding)
   void* C = nullptr;                    // [batch][M][ldc] bf16 or f32
   int M = 0, N = 0, K = 0, Nw = 0;
-  int lda = 0, ldc = 0;
+  int lda = 0, ldc = 0, ldw = 0;      // ldw = W row stride (0 -> K)
   long long sA = 0, sW = 0, sC = 0;
   int batch = 1;
   float alpha = 1.f;
