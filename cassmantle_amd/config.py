@@ -41,6 +41,7 @@ class GameConfig:
     time_per_prompt: int = 900            # main.py:23 (Server default 600 overridden)
     min_score: float = 0.01               # src/server.py:17
     max_retries: int = 5                  # src/backend.py:23
+    retry_backoff: float = 0.5            # s; reference sleeps 10*(retry+1) s on HTTP 503 (src/utils.py:57)
     lock_timeout: float = 120.0           # src/backend.py:47
     acquire_timeout: float = 2.0          # src/backend.py:48
     num_masked: int = 2                   # src/backend.py:49

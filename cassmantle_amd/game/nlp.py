@@ -50,11 +50,12 @@ def word_tokenize(text: str) -> List[str]:
 
 
 def reconstruct_sentence(tokens: Sequence[str]) -> str:
-    """Inverse of :func:`word_tokenize` for display (``src/utils.py:18-26`` parity: no space
-    before punctuation, hyphen- and apostrophe-tokens)."""
+    """Inverse of :func:`word_tokenize` for display.  The reference (``src/utils.py:18-26``)
+    also glues hyphenated words to their predecessor; here only punctuation and contraction
+    tokens (``n't``, ``'s``, ...) attach without a space."""
     out = ""
     for tok in tokens:
-        if (len(tok) == 1 and not tok.isalnum()) or "-" in tok or "'" in tok:
+        if (len(tok) == 1 and not tok.isalnum() and tok not in "(`") or tok.startswith("'") or tok.lower() == "n't":
             out += tok
         else:
             out += " " + tok

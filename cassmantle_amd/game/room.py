@@ -107,7 +107,9 @@ class GameRoom:
                 except Exception as e:  # noqa: BLE001 - mirror reference's broad handling
                     log.error("[ERROR] prompt generation failed: %s", e)
                 if attempt + 1 < self.cfg.max_retries:
-                    await self.clock.sleep(0.01 * (attempt + 1))
+                    # linear backoff like api_call (src/utils.py:57), in wall time: a
+                    # generator failure is not a function of the game clock
+                    await asyncio.sleep(self.cfg.retry_backoff * (attempt + 1))
             return None
         finally:
             self.store.hset(self.k("prompt"), "status", "idle")
@@ -127,7 +129,9 @@ class GameRoom:
                 except Exception as e:  # noqa: BLE001
                     log.error("[ERROR] image generation failed: %s", e)
                 if attempt + 1 < self.cfg.max_retries:
-                    await self.clock.sleep(0.01 * (attempt + 1))
+                    # linear backoff like api_call (src/utils.py:57), in wall time: a
+                    # generator failure is not a function of the game clock
+                    await asyncio.sleep(self.cfg.retry_backoff * (attempt + 1))
             return None
         finally:
             self.store.hset(self.k("image"), "status", "idle")

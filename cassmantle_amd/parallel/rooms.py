@@ -1,0 +1,275 @@
+"""Data-parallel room sharding across the GPUs of a node (BASELINE configs 3 and 5).
+
+The reference serves ONE global room and scales only by uvicorn workers that race for Redis
+locks (``src/backend.py:83,155,206``).  Here rooms are sharded over one process
+per GPU: room ``i`` (in a fixed room order) is owned by rank ``i mod W``.  Generation is
+organised in *generation rounds* driven by rank 0 (the front-end's rank):
+
+  C1  rank 0 broadcasts the job list (room, styled prompt, seed) — a few hundred bytes;
+      every rank derives the same ownership table, so no further negotiation is needed;
+      each rank runs ONE batched pipeline call for all images of the rooms it owns;
+  C2  the uint8 images are gathered to rank 0 (768 KiB per 512² image, padded to the
+      per-rank maximum so the collective has static shapes);
+  C4  a barrier closes the round.
+
+Every message is latency-bound (≤ a few MB), so the protocol uses a fixed, tiny number of
+collectives per round and never sits inside the denoise loop.  With ``backend="nccl"`` these
+are RCCL collectives over xGMI; CPU tests run the identical code on gloo.
+
+Failure handling: every rank publishes a heartbeat in the process-group store;
+rank 0's :class:`HeartbeatMonitor` reports ranks whose heartbeat is stale and the sharding
+reassigns their rooms to live ranks; a generation round that raises is reported as failed
+so the affected rooms keep their current content (the reference's "round repeats" fallback).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..game.content import ImageGenerationError, ImageGenerator
+from .dist import DistContext, broadcast_object
+
+log = logging.getLogger("cassmantle")
+
+
+class RoomSharding:
+    """room -> owner rank, with reassignment away from dead ranks."""
+
+    def __init__(self, room_ids: Sequence[str], world: int) -> None:
+        self.room_ids = list(room_ids)
+        self.world = world
+        self.dead: Set[int] = set()
+        self._table = self._build()
+
+    def _build(self) -> Dict[str, int]:
+        live = [r for r in range(self.world) if r not in self.dead] or [0]
+        return {rid: live[i % len(live)] for i, rid in enumerate(self.room_ids)}
+
+    def owner(self, room: str) -> int:
+        return self._table[room]
+
+    def rooms_of(self, rank: int) -> List[str]:
+        return [r for r in self.room_ids if self._table[r] == rank]
+
+    def mark_dead(self, ranks: Iterable[int]) -> None:
+        self.dead |= set(ranks)
+        self._table = self._build()
+
+    def state(self) -> Tuple[int, ...]:
+        return tuple(sorted(self.dead))
+
+
+@dataclass
+class GenJob:
+    room: str
+    prompt: str
+    seed: int
+
+
+STOP = "__stop__"
+
+
+class RankWorker:
+    """Executes generation rounds; identical code on every rank."""
+
+    def __init__(self, ctx: DistContext, generator: ImageGenerator, sharding: RoomSharding,
+                 negative_prompt: str = "blurry, distorted, fake, abstract, negative") -> None:
+        self.ctx = ctx
+        self.gen = generator
+        self.sharding = sharding
+        self.negative = negative_prompt
+        self.res = generator.resolution
+        self.rounds = 0
+
+    def _device(self) -> torch.device:
+        return self.ctx.device if self.ctx.backend == "nccl" else torch.device("cpu")
+
+    def run_round(self, jobs: Optional[List[GenJob]]) -> Optional[Dict[Tuple[str, int], np.ndarray]]:
+        """Collective: every rank must call it.  Rank 0 passes the job list (or STOP); others
+        pass None.  Returns {(room, job_index): image} on rank 0, None elsewhere; returns the
+        string STOP on every rank when the loop should end."""
+        msg = broadcast_object((jobs, self.sharding.state()) if self.ctx.rank == 0 else None)   # C1
+        jobs, dead = msg
+        if jobs == STOP:
+            return STOP  # type: ignore[return-value]
+        if tuple(sorted(self.sharding.dead)) != tuple(dead):
+            self.sharding.mark_dead(dead)
+        W, rank = self.ctx.world_size, self.ctx.rank
+        owners = [self.sharding.owner(j.room) for j in jobs]
+        per_rank = [[i for i, o in enumerate(owners) if o == r] for r in range(W)]
+        jmax = max((len(p) for p in per_rank), default=0)
+        mine = per_rank[rank]
+        dev = self._device()
+        H = self.res
+        buf = torch.zeros((max(jmax, 1), H, H, 3), dtype=torch.uint8, device=dev)
+        ok = torch.zeros((max(jmax, 1),), dtype=torch.uint8, device=dev)
+        if mine:
+            try:
+                imgs = self.gen.generate([jobs[i].prompt for i in mine], self.negative, [jobs[i].seed for i in mine])
+                for k, im in enumerate(imgs):
+                    t = torch.from_numpy(np.ascontiguousarray(im)) if isinstance(im, np.ndarray) else im
+                    buf[k].copy_(t.to(dev))
+                    ok[k] = 1
+            except Exception as e:  # noqa: BLE001 - a failed rank must still join the collectives
+                log.error("[ERROR] rank %d generation failed: %s", rank, e)
+        out = None
+        if W > 1:
+            if rank == 0:
+                gl = [torch.empty_like(buf) for _ in range(W)]
+                gk = [torch.empty_like(ok) for _ in range(W)]
+                dist.gather(buf, gl, dst=0)                                             # C2
+                dist.gather(ok, gk, dst=0)
+            else:
+                dist.gather(buf, None, dst=0)
+                dist.gather(ok, None, dst=0)
+                gl = gk = None
+            dist.barrier()                                                              # C4
+        else:
+            gl, gk = [buf], [ok]
+        if rank == 0:
+            out = {}
+            for r in range(W):
+                host = gl[r].cpu().numpy()
+                flags = gk[r].cpu().numpy()
+                for k, i in enumerate(per_rank[r]):
+                    if flags[k]:
+                        out[(jobs[i].room, i)] = host[k]
+        self.rounds += 1
+        return out
+
+    def serve_forever(self) -> None:
+        """Non-zero ranks: follow rank 0's rounds until STOP."""
+        while True:
+            if self.run_round(None) == STOP:
+                return
+
+
+class GenerationCoordinator:
+    """Rank 0: turns per-room ``generate`` calls (from the game rooms' worker threads) into
+    batched generation rounds, executed on ONE dedicated thread (all collectives are issued
+    from that thread, in order)."""
+
+    def __init__(self, worker: RankWorker, window_s: float = 0.5) -> None:
+        self.worker = worker
+        self.window = window_s
+        self._q: "queue.Queue" = queue.Queue()
+        self._thread = threading.Thread(target=self._loop, name="gen-coordinator", daemon=True)
+        self._stopped = False
+        self._thread.start()
+
+    def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
+        fut: cf.Future = cf.Future()
+        self._q.put((room, list(prompts), list(seeds), fut))
+        return fut
+
+    def _loop(self) -> None:
+        while True:
+            item = self._q.get()
+            if item is None:
+                break
+            batch = [item]
+            t_end = time.monotonic() + self.window
+            while True:
+                rem = t_end - time.monotonic()
+                if rem <= 0:
+                    break
+                try:
+                    nxt = self._q.get(timeout=rem)
+                except queue.Empty:
+                    break
+                if nxt is None:
+                    self._q.put(None)
+                    break
+                batch.append(nxt)
+            jobs: List[GenJob] = []
+            spans = []
+            for room, prompts, seeds, fut in batch:
+                start = len(jobs)
+                jobs.extend(GenJob(room, p, s) for p, s in zip(prompts, seeds))
+                spans.append((start, len(jobs), room, fut))
+            try:
+                res = self.worker.run_round(jobs)
+                for s, e, room, fut in spans:
+                    imgs = [res.get((room, i)) for i in range(s, e)]
+                    if any(im is None for im in imgs):
+                        fut.set_exception(ImageGenerationError(f"room {room}: generation failed"))
+                    else:
+                        fut.set_result(imgs)
+            except Exception as e:  # noqa: BLE001
+                for *_, fut in spans:
+                    if not fut.done():
+                        fut.set_exception(e)
+        self.worker.run_round(STOP)  # type: ignore[arg-type]
+
+    def close(self) -> None:
+        if not self._stopped:
+            self._stopped = True
+            self._q.put(None)
+            self._thread.join(timeout=60)
+
+
+class RankImageGenerator(ImageGenerator):
+    """Game-layer generator for one room: forwards to the room's owner rank."""
+
+    def __init__(self, coordinator: GenerationCoordinator, room: str, timeout_s: float = 900.0) -> None:
+        self.coord = coordinator
+        self.room = room
+        self.resolution = coordinator.worker.res
+        self.timeout = timeout_s
+
+    def generate(self, prompts, negative_prompt, seeds):
+        return self.coord.submit(self.room, prompts, seeds).result(timeout=self.timeout)
+
+
+class HeartbeatMonitor:
+    """Per-rank heartbeat in the process-group store; rank 0 lists stale ranks."""
+
+    def __init__(self, store, rank: int, world: int, period_s: float = 1.0, stale_s: float = 10.0) -> None:
+        self.store, self.rank, self.world = store, rank, world
+        self.period, self.stale = period_s, stale_s
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._beat, daemon=True)
+
+    def start(self) -> "HeartbeatMonitor":
+        self.beat()
+        self._t.start()
+        return self
+
+    def beat(self) -> None:
+        self.store.set(f"hb/{self.rank}", repr(time.time()))
+
+    def _beat(self) -> None:
+        while not self._stop.wait(self.period):
+            try:
+                self.beat()
+            except Exception:  # noqa: BLE001
+                return
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    def dead_ranks(self, now: Optional[float] = None) -> List[int]:
+        now = now or time.time()
+        dead = []
+        for r in range(self.world):
+            try:
+                key = f"hb/{r}"
+                if not self.store.check([key]):   # get() would block until the key exists
+                    dead.append(r)
+                    continue
+                ts = float(self.store.get(key).decode())
+            except Exception:  # noqa: BLE001
+                dead.append(r)
+                continue
+            if now - ts > self.stale:
+                dead.append(r)
+        return dead
