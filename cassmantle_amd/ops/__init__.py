@@ -97,6 +97,13 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return ref.conv2d(x, w, bias, stride, padding, residual, upsample, chan_bias)
     B, H, W, Cin = x.shape
     Cout, kh, kw, _ = w.shape
+    if Cin % 8 != 0:
+        # 4-channel latents (conv_in): zero-pad channels to 8 so the MFMA path's 16-byte
+        # k-chunks apply (the extra K is zeros on both operands)
+        pad = 8 - Cin % 8
+        x = torch.nn.functional.pad(x, (0, pad))
+        w = torch.nn.functional.pad(w, (0, pad))
+        Cin += pad
     Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
     Ho = (Hi + 2 * padding - kh) // stride + 1
     Wo = (Wi + 2 * padding - kw) // stride + 1

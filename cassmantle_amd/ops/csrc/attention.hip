@@ -182,24 +182,29 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f((m_run - m_new) * c);
     const float mc = m_new * c;
     float rs = 0.f;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = exp2f(fmaf(sacc[hf][r], c, -mc));
+        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
         sacc[hf][r] = pv;
         rs += pv;
       }
     rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
+    // rescale O only when some query's running max grew (wave-uniform branch; after the
+    // first few tiles the max rarely moves, so the O-wide multiply is usually skipped)
+    if (!__all(m_new == m_run)) {
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < NDC; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+    }
+    l_run += rs;
     m_run = m_new;
-#pragma unroll
-    for (int i = 0; i < NDC; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
 
     // ---- P^T fragments (bf16), k-step kk = 2*hf + s uses regs 8s..8s+7 of sacc[hf]
     bf16x8_t pf[4];

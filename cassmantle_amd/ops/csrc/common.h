@@ -17,15 +17,17 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 CM_DEVICE float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
-// round-to-nearest-even f32 -> bf16 (NaN preserved: quiet bit forced)
-CM_DEVICE uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
-CM_DEVICE uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+// f32 -> bf16, round-to-nearest-even.  A plain cast lowers to the gfx950 hardware converter
+// (v_cvt_pk_bf16_f32, NaN-preserving; MI355X_MICROARCH.md 'Correctness boundaries').
+CM_DEVICE uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// two floats -> one packed dword in ONE v_cvt_pk_bf16_f32
+CM_DEVICE uint32_t pack2(float a, float b) {
+  bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
 
 CM_DEVICE void unpack8(const uint4& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);

@@ -80,30 +80,35 @@ __global__ void gn_partial_kernel(const uint16_t* __restrict__ x, float* __restr
   }
 }
 
+// one 64-thread block per (b, group): the chunks x Cg partials are summed in fp64 across lanes
 __global__ void gn_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ gamma,
                                    const uint16_t* __restrict__ beta, float* __restrict__ scale,
                                    float* __restrict__ shift, long long S, int C, int G, int chunks, float eps) {
-  const int b = blockIdx.x;
+  const int g = blockIdx.x, b = blockIdx.y;
   const int Cg = C / G;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double sum = 0.0, sq = 0.0;
-    for (int ck = 0; ck < chunks; ++ck)
-      for (int c = 0; c < Cg; ++c) {
-        int ch = g * Cg + c;
-        sum += part[(((long long)b * chunks + ck) * 2 + 0) * C + ch];
-        sq += part[(((long long)b * chunks + ck) * 2 + 1) * C + ch];
-      }
-    double n = (double)S * Cg;
-    double mean = sum / n;
-    double var = sq / n - mean * mean;
-    if (var < 0) var = 0;
-    float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    for (int c = 0; c < Cg; ++c) {
-      int ch = g * Cg + c;
-      float ga = bf2f(gamma[ch]), be = bf2f(beta[ch]);
-      scale[b * C + ch] = ga * rstd;
-      shift[b * C + ch] = be - (float)mean * ga * rstd;
-    }
+  const int lane = threadIdx.x;
+  double sum = 0.0, sq = 0.0;
+  for (int j = lane; j < chunks * Cg; j += 64) {
+    const int ck = j / Cg, c = j - ck * Cg;
+    const int ch = g * Cg + c;
+    sum += part[(((long long)b * chunks + ck) * 2 + 0) * C + ch];
+    sq += part[(((long long)b * chunks + ck) * 2 + 1) * C + ch];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sum += __shfl_xor(sum, o, 64);
+    sq += __shfl_xor(sq, o, 64);
+  }
+  const double n = (double)S * Cg;
+  const double mean = sum / n;
+  double var = sq / n - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int c = lane; c < Cg; c += 64) {
+    const int ch = g * Cg + c;
+    const float ga = bf2f(gamma[ch]), be = bf2f(beta[ch]);
+    scale[b * C + ch] = ga * rstd;
+    shift[b * C + ch] = be - (float)mean * ga * rstd;
   }
 }
 
@@ -211,7 +216,7 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
     hipLaunchKernelGGL(gn_partial_kernel<1>, g1, dim3(GN_THREADS), sh, s, x, part, S, C, chunks, rpc);
   else
     hipLaunchKernelGGL(gn_partial_kernel<2>, g1, dim3(GN_THREADS), sh, s, x, part, S, C, chunks, rpc);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(64), 0, s, part, gamma, beta, scale, shift, S, C, G, chunks, eps);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(G, B), dim3(64), 0, s, part, gamma, beta, scale, shift, S, C, G, chunks, eps);
   long long nvec = (long long)B * S * C / 8;
   long long blocks = (nvec + 255) / 256;
   if (blocks > 4096) blocks = 4096;
