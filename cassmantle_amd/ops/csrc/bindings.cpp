@@ -25,6 +25,18 @@ const uint16_t* opt_bptr(const c10::optional<at::Tensor>& t) {
   return bptr(*t);
 }
 
+// plans split-K and allocates its fp32 partial slabs from the caching allocator (graph-pool
+// safe inside a capture), then launches on the current stream
+void run_gemm(GemmArgs& p, const at::Tensor& like) {
+  p.split = gemm_plan_split(p);
+  if (p.split > 1) {
+    auto ws = at::empty({(long long)p.split * p.M * p.N}, like.options().dtype(at::kFloat));
+    launch_gemm(p, ws.data_ptr<float>(), cur_stream());
+  } else {
+    launch_gemm(p, nullptr, cur_stream());
+  }
+}
+
 void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
@@ -48,7 +60,7 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     CHECK_BF16(out);
   }
   p.C = out.data_ptr();
-  launch_gemm(p, cur_stream());
+  run_gemm(p, out);
 }
 
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -74,7 +86,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   if (chan_bias.has_value() && chan_bias->defined())
     TORCH_CHECK(chan_bias->numel() == x.size(0) * p.N, "conv2d: chan_bias must be [B, Cout]");
   p.C = out.data_ptr();
-  launch_gemm(p, cur_stream());
+  run_gemm(p, out);
 }
 
 // batched C[b] = alpha * A[b] @ B[b]^T ; A [Bt, M, K] (row stride free), B [Bt, N, K], C [Bt, M, N]
@@ -95,7 +107,7 @@ void bmm_nt(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, double al
     CHECK_BF16(out);
   }
   p.C = out.data_ptr();
-  launch_gemm(p, cur_stream());
+  run_gemm(p, out);
 }
 
 void group_norm(const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& out,

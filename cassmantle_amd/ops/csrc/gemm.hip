@@ -10,17 +10,26 @@
 // * W rows are K-contiguous ([Cout][kh][kw][Cin] for convs), so both operands are read from
 //   LDS as 16-byte k-chunks: mfma_f32_16x16x32_bf16 fragments straight from ds_read_b128.
 // * Global -> LDS by LDS-DMA (global_load_lds_dwordx4, cdna_hip_programming.md §5): no VGPR
-//   staging, no ds_write; each wave-instruction fills 8 rows x 128 B.  The next k-tile's DMA is
-//   issued before the current tile's MFMAs into the other of two LDS buffers; one barrier per
-//   k-tile.  Out-of-range rows / conv padding point their lane at a 16-byte zero page.
+//   staging, no ds_write; each wave-instruction fills 8 rows x 128 B.  Out-of-range rows and
+//   conv padding point their lane at a 16-byte zero page.
+//   - STAGES=2: the next k-tile's DMA is issued before the current tile's MFMAs; one
+//     __syncthreads (= vmcnt(0) + barrier) per k-tile.
+//   - STAGES=3: two tiles in flight; a counted `s_waitcnt vmcnt(N)` retires only the tile about
+//     to be read and a raw s_barrier publishes it, so one DMA stays in flight across every
+//     barrier ("Pipelining across barriers", guide §5).
 // * LDS rows are 128 B; logical chunk c of row r lives in slot c ^ ((r >> 1) & 7).  The DMA
 //   image is lane-linear, so the swizzle is applied on the SOURCE address (rule 21) and the
 //   same XOR on the ds_read; each 16-lane ds_read_b128 group then hits 16 distinct bank slots.
 // * Tiles (BM x BN x 64, 4 waves as WM x WN): 128x128 (2x2), 256x64 (4x1) for N = 64 (mod
 //   128), 256x16 (4x1) for the 3/4-channel conv_out layers.
+// * Split-K: grids that cannot fill the 256 CUs (the 16x16 / 8x8 UNet levels: M = 2048 / 512
+//   with K = 11520) split the k-tiles over blockIdx.y; fp32 partial slabs are summed by a
+//   second kernel that applies the epilogue (cheaper than a sub-occupied chip).
 // * GEGLU (transformer FF): W tile rows interleave 16-row value/gate blocks, so each lane
 //   holds h and g of the same output column and computes h * gelu(g) in registers.
 // * Block ids are remapped XCD-aware so tiles that share an A panel run on one XCD's L2.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -39,8 +48,55 @@ CM_DEVICE void glds16(const void* src, uint4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32>
-__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
+template <int N>
+CM_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+CM_DEVICE void add4(float* o, uint2 v) {
+  o[0] += bf2f(v.x & 0xffff); o[1] += bf2f(v.x >> 16); o[2] += bf2f(v.y & 0xffff); o[3] += bf2f(v.y >> 16);
+}
+
+// epilogue for 4 consecutive output columns n..n+3 of row m (raw accumulators in o)
+template <bool OUTF32>
+CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
+  const int hw = p.Ho * p.Wo;
+  const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
+  const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
+  if (full) {
+    if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
+    if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * p.N + n));
+    if (p.act != ACT_NONE) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
+    }
+    if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
+    if constexpr (OUTF32) {
+      float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
+      *reinterpret_cast<float4*>(C) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+      uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
+      *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+    }
+  } else {   // ragged N (3-channel conv_out): element-wise tail
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= p.N) break;
+      float v = o[r];
+      if (p.bias) v += bf2f(p.bias[n + r]);
+      if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * p.N + n + r]);
+      v = apply_act(v, p.act);
+      if (p.residual) v += bf2f(p.residual[(long long)m * p.ldc + n + r]);
+      if constexpr (OUTF32)
+        reinterpret_cast<float*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = v;
+      else
+        reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = f2bf(v);
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES>
+__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
   static_assert(WM * WN == 4, "4 waves");
@@ -49,6 +105,8 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
   static_assert(!GEGLU || (TI % 2 == 0), "geglu pairs");
   constexpr int AR = BM / 32;              // A DMA rounds (32 rows each, 8 per wave)
   constexpr int WR = (BN + 31) / 32;       // W DMA rounds
+  static_assert(STAGES == 2 || (STAGES == 3 && BN % 32 == 0), "counted waits need equal DMA per wave");
+  constexpr int NPT = AR + WR;             // DMA instructions per wave per k-tile
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -158,16 +216,10 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
-  stage(0, 0);
-  __syncthreads();   // drains the DMA (vmcnt(0)) and publishes the tile
-
   const int fr = lane & 15;      // fragment row within 16
   const int fq = lane >> 4;      // k-chunk within a 32-k step
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const uint4* As = smem + cur * TILE;
+  auto compute = [&](int buf) {
+    const uint4* As = smem + buf * TILE;
     const uint4* Ws = As + BM * 8;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -189,16 +241,39 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();   // next tile landed (vmcnt(0)) and everyone is done with this one
+  };
+
+  // ---- k range of this split
+  const int nk_all = (p.K + BK - 1) / BK;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+
+  if constexpr (STAGES == 2) {
+    if (nk > 0) stage(kt0, 0);
+    __syncthreads();                       // drains the DMA (vmcnt(0)) and publishes the tile
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) stage(kt0 + t + 1, (t + 1) & 1);
+      compute(t & 1);
+      __syncthreads();                     // next tile landed and everyone is done with this one
+    }
+  } else {
+    if (nk > 0) stage(kt0, 0);
+    if (nk > 1) stage(kt0 + 1, 1);
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) wait_vmcnt<NPT>();   // retire tile t, leave tile t+1 in flight
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();        // every wave's share of tile t landed; tile t-1 is free
+      if (t + 2 < nk) stage(kt0 + t + 2, (t + 2) % 3);
+      compute(t % 3);
+    }
   }
 
   // ---- epilogue
-  const int hw = p.Ho * p.Wo;
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int m = m0 + wm * (BM / WM) + 16 * j + fr;
     if (m >= p.M) continue;
-    const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
     if constexpr (GEGLU) {
 #pragma unroll
       for (int pi = 0; pi < TI / 2; ++pi) {
@@ -212,10 +287,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
           o[r] = h * gelu_f(g);
         }
         uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-        if (p.residual) {
-          uint2 rv = *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n);
-          o[0] += bf2f(rv.x & 0xffff); o[1] += bf2f(rv.x >> 16); o[2] += bf2f(rv.y & 0xffff); o[3] += bf2f(rv.y >> 16);
-        }
+        if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
         *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       }
     } else {
@@ -223,51 +295,30 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
       for (int i = 0; i < TI; ++i) {
         const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
         if (n >= p.N) continue;
-        const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0);
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] * p.alpha;
-        if (full) {
-          if (p.bias) {
-            uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
-            o[0] += bf2f(bv.x & 0xffff); o[1] += bf2f(bv.x >> 16); o[2] += bf2f(bv.y & 0xffff); o[3] += bf2f(bv.y >> 16);
-          }
-          if (p.chan_bias) {
-            uint2 bv = *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * p.N + n);
-            o[0] += bf2f(bv.x & 0xffff); o[1] += bf2f(bv.x >> 16); o[2] += bf2f(bv.y & 0xffff); o[3] += bf2f(bv.y >> 16);
-          }
-          if (p.act != ACT_NONE) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
-          }
-          if (p.residual) {
-            uint2 rv = *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n);
-            o[0] += bf2f(rv.x & 0xffff); o[1] += bf2f(rv.x >> 16); o[2] += bf2f(rv.y & 0xffff); o[3] += bf2f(rv.y >> 16);
-          }
-          if constexpr (OUTF32) {
-            float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-            *reinterpret_cast<float4*>(C) = make_float4(o[0], o[1], o[2], o[3]);
-          } else {
-            uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-            *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          }
-        } else {   // ragged N (3-channel conv_out): element-wise tail
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (n + r >= p.N) break;
-            float v = o[r];
-            if (p.bias) v += bf2f(p.bias[n + r]);
-            if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * p.N + n + r]);
-            v = apply_act(v, p.act);
-            if (p.residual) v += bf2f(p.residual[(long long)m * p.ldc + n + r]);
-            if constexpr (OUTF32)
-              reinterpret_cast<float*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = v;
-            else
-              reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = f2bf(v);
-          }
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (gridDim.y > 1) {               // split-K: raw fp32 partial slab
+          float* dst = partial + ((long long)blockIdx.y * p.M + m) * p.N + n;
+          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+          epilogue4<OUTF32>(p, batch, m, n, o);
         }
       }
     }
+  }
+}
+
+template <bool OUTF32>
+__global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ partial, int split) {
+  const long long nq = (long long)p.M * (p.N / 4);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / (p.N / 4));
+    const int n = (int)(i - (long long)m * (p.N / 4)) * 4;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < split; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + ((long long)s * p.M + m) * p.N + n);
+      o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
+    }
+    epilogue4<OUTF32>(p, 0, m, n, o);
   }
 }
 
@@ -314,41 +365,83 @@ __global__ void gemm_simt_kernel(GemmArgs p) {
     reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n] = f2bf(o);
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32>
-void launch_t(const GemmArgs& p, hipStream_t s) {
+int g_stages_override = -1;   // CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark)
+
+int stages_pref() {
+  if (g_stages_override < 0) {
+    const char* e = getenv("CASSMANTLE_GEMM_STAGES");
+    g_stages_override = e ? atoi(e) : 0;
+  }
+  return g_stages_override;
+}
+
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES>
+void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
-  dim3 grid(nN * nM, 1, p.batch);
-  constexpr size_t lds = 2 * (size_t)(BM + BN) * BK * 2;
+  const int split = (ws != nullptr && p.split > 1) ? p.split : 1;
+  dim3 grid(nN * nM, split, p.batch);
+  constexpr size_t lds = (size_t)STAGES * (BM + BN) * BK * 2;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
     static const bool once = [] {
-      (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32>,
+      (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return true;
     }();
     (void)once;
   }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32>), grid, dim3(THREADS), lds, s, p);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES>), grid, dim3(THREADS), lds, s, p, ws);
+  if (split > 1) {
+    const long long nq = (long long)p.M * (p.N / 4);
+    const long long nb = (nq + 255) / 256;
+    const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel<OUTF32>, dim3(rb), dim3(256), 0, s, p, ws, split);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32>
+void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
+  if constexpr (BN % 32 == 0) {
+    if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3>(p, ws, s);
+  }
+  launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2>(p, ws, s);
 }
 
 template <int CONV, bool OUTF32>
-void launch_shape(const GemmArgs& p, hipStream_t s) {
-  if (p.N <= 16) launch_t<256, 16, 4, 1, CONV, false, OUTF32>(p, s);
-  else if (p.N % 128 != 0 && p.N % 64 == 0) launch_t<256, 64, 4, 1, CONV, false, OUTF32>(p, s);
-  else launch_t<128, 128, 2, 2, CONV, false, OUTF32>(p, s);
+void launch_shape(const GemmArgs& p, float* ws, hipStream_t s) {
+  if (p.N <= 16) launch_st<256, 16, 4, 1, CONV, false, OUTF32>(p, ws, s);
+  else if (p.N % 128 != 0 && p.N % 64 == 0) launch_st<256, 64, 4, 1, CONV, false, OUTF32>(p, ws, s);
+  else launch_st<128, 128, 2, 2, CONV, false, OUTF32>(p, ws, s);
 }
 
 template <int CONV>
-void launch_tiles(const GemmArgs& p, hipStream_t s) {
-  if (p.act == ACT_GEGLU) launch_t<128, 128, 2, 2, CONV, true, false>(p, s);
-  else if (p.out_f32) launch_shape<CONV, true>(p, s);
-  else launch_shape<CONV, false>(p, s);
+void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
+  if (p.act == ACT_GEGLU) launch_st<128, 128, 2, 2, CONV, true, false>(p, ws, s);
+  else if (p.out_f32) launch_shape<CONV, true>(p, ws, s);
+  else launch_shape<CONV, false>(p, ws, s);
 }
 
 }  // namespace
 
-void launch_gemm(const GemmArgs& p, hipStream_t s) {
+int gemm_plan_split(const GemmArgs& p) {
+  // split-K only for grids that cannot fill the chip and have a long K loop; mirrors the
+  // tile choice of launch_shape (GEGLU / batched / ragged shapes never split)
+  if (p.batch != 1 || p.act == ACT_GEGLU || p.N % 4 != 0 || p.K % 8 != 0) return 1;
+  if (p.conv && p.Cin % 8 != 0) return 1;
+  const bool mid = (p.N > 16) && (p.N % 128 != 0 && p.N % 64 == 0);
+  const int BM = (p.N <= 16 || mid) ? 256 : 128;
+  const int BN = p.N <= 16 ? 16 : (mid ? 64 : 128);
+  const long long blocks = (long long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  const int nk = (p.K + BK - 1) / BK;
+  if (blocks >= 256 || nk < 16) return 1;
+  int split = (int)((512 + blocks - 1) / blocks);
+  split = min(split, nk / 4);
+  split = min(split, GEMM_MAX_SPLIT);
+  return split < 2 ? 1 : split;
+}
+
+void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
   const bool mfma_ok = (p.K % 8 == 0) && (!p.conv || p.Cin % 8 == 0) &&
                        (p.conv || p.lda % 8 == 0) && (p.ldw % 8 == 0);
   if (!mfma_ok) {
@@ -361,7 +454,7 @@ void launch_gemm(const GemmArgs& p, hipStream_t s) {
       hipLaunchKernelGGL(gemm_simt_kernel<0>, grid, dim3(256), 0, s, p);
     return;
   }
-  if (!p.conv) launch_tiles<0>(p, s);
-  else if (p.Cin % 64 == 0) launch_tiles<2>(p, s);
-  else launch_tiles<1>(p, s);
+  if (!p.conv) launch_tiles<0>(p, ws, s);
+  else if (p.Cin % 64 == 0) launch_tiles<2>(p, ws, s);
+  else launch_tiles<1>(p, ws, s);
 }
