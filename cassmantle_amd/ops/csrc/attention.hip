@@ -58,7 +58,9 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   const int ql = lane & 31;
 
   const int nqb = (a.Nq + QB - 1) / QB;
-  const int bid = blockIdx.x;
+  // XCD-aware order: the q-blocks of one (batch, head) run on one XCD, so its K/V (<= 1 MB)
+  // is fetched into that XCD's L2 once instead of once per XCD
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb;
   const int bh = bid / nqb;
   const int h = bh % a.H;
@@ -93,6 +95,10 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
   const float c = a.scale * 1.4426950408889634f;
+  // padded head dims (40 -> 64, 80 -> 96): the first padding column of V carries ones, so the
+  // row sum of P comes out of the P.V MFMAs (rescaled with O for free) instead of 32 VALU adds
+  // and a cross-half shuffle per tile
+  constexpr bool ones = DO > DQK;   // d <= DQK < DO: at least one zero-padded V column
 
   uint4 kr[KLD], vr[VLD];
   auto gload = [&](int t) {
@@ -113,6 +119,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (key < KT && kbase + key < nk && ch * 8 < d)
         v = *reinterpret_cast<const uint4*>(Vp + (long long)(kbase + key) * a.v_sn + ch * 8);
+      else if (ones && ch * 8 == d)
+        v.x = 0x3F80u;   // V[:, d] = 1.0: the P.V MFMA accumulates the softmax row sum in O^T row d
       vr[i] = v;
     }
   };
@@ -184,15 +192,22 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
     const float m_new = fmaxf(m_run, mx);
     const float mc = m_new * c;
     float rs = 0.f;
+    if constexpr (ones) {
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
+      for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
-        sacc[hf][r] = pv;
-        rs += pv;
-      }
-    rs += __shfl_xor(rs, 32, 64);
+        for (int r = 0; r < 16; ++r) sacc[hf][r] = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
+    } else {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pv = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
+          sacc[hf][r] = pv;
+          rs += pv;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+    }
     // rescale O only when some query's running max grew (wave-uniform branch; after the
     // first few tiles the max rarely moves, so the O-wide multiply is usually skipped)
     if (!__all(m_new == m_run)) {
@@ -245,6 +260,17 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l
+  if constexpr (ones) {
+    // row sum sits in O^T row d: chunk d/32, register 4*((d%32)/8) of the lane half 0
+    const int dcl = d >> 5, rgl = ((d & 31) >> 3) << 2;
+    float ls = 0.f;
+#pragma unroll
+    for (int dc = 0; dc < NDC; ++dc)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4)
+        if (dc == dcl && r == rgl) ls = oacc[dc][r];
+    l_run = __shfl(ls, ql, 64);
+  }
   if (q < a.Nq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     uint16_t* Op = a.o + (long long)b * a.o_sb + (long long)q * a.o_sn + (long long)h * a.o_sh;
@@ -276,7 +302,9 @@ template <int DQK, int DO>
 void launch_nw(const AttnArgs& a, hipStream_t s) {
   // enough workgroups to fill 256 CUs: fall back to fewer waves per block for short sequences
   long long blocks4 = (long long)((a.Nq + 127) / 128) * a.H * a.B;
-  if (blocks4 >= 512) launch_t<DQK, DO, 4>(a, s);
+  long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
+  if (DO <= 96 && blocks8 >= 1024) launch_t<DQK, DO, 8>(a, s);   // 8 waves share each K/V tile
+  else if (blocks4 >= 512) launch_t<DQK, DO, 4>(a, s);
   else launch_t<DQK, DO, 2>(a, s);
 }
 
