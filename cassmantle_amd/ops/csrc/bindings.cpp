@@ -28,7 +28,9 @@ const uint16_t* opt_bptr(const c10::optional<at::Tensor>& t) {
 // plans split-K and allocates its fp32 partial slabs from the caching allocator (graph-pool
 // safe inside a capture), then launches on the current stream
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
-  p.split = gemm_plan_split(p);
+  const GemmPlan plan = gemm_plan(p);
+  p.cfg = plan.cfg;
+  p.split = plan.split;
   if (p.split > 1) {
     auto ws = at::empty({(long long)p.split * p.M * p.N}, like.options().dtype(at::kFloat));
     launch_gemm(p, ws.data_ptr<float>(), cur_stream());

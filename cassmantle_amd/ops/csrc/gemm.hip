@@ -129,23 +129,33 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
   // ---- this lane's DMA rows: round i covers rows 32i + 8*wave + (lane>>3), slot lane&7
   const int slot = lane & 7;
   const int rsub = 8 * wave + (lane >> 3);
-  int a_row[AR], a_chunk[AR];
-  int cb_[AR], cy_[AR], cx_[AR];
+  // Per-row state is computed ONCE; the per-k-tile address work is then a few VALU ops per DMA
+  // (the first version recomputed divisions per tile and was issue-bound on SALU/VALU:
+  // 15 SALU + 9 VALU per MFMA in the rocprof counters).
+  int a_chunk[AR];
+  long long a_off[AR];       // plain: row*lda + chunk*8 ; conv: element offset of pixel (b,cy,cx) + chunk*8
+  int cy_[AR], cx_[AR], cbh_[AR];
+  bool a_ok[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int r = 32 * i + rsub;
-    a_row[i] = m0 + r;
+    const int row = m0 + r;
     a_chunk[i] = slot ^ ((r >> 1) & 7);
-    if constexpr (CONV != 0) {
-      const int m = a_row[i] < p.M ? a_row[i] : 0;
+    a_ok[i] = row < p.M;
+    if constexpr (CONV == 0) {
+      a_off[i] = (long long)row * p.lda + a_chunk[i] * 8;
+    } else {
+      const int m = a_ok[i] ? row : 0;
       const int hw = p.Ho * p.Wo;
       const int b = m / hw;
       const int rr = m - b * hw;
       const int oy = rr / p.Wo;
       const int ox = rr - oy * p.Wo;
-      cb_[i] = b;
       cy_[i] = oy * p.stride - p.pad;
       cx_[i] = ox * p.stride - p.pad;
+      cbh_[i] = b * p.IH;
+      a_off[i] = (((long long)b * p.IH + cy_[i]) * p.IW + cx_[i]) * p.Cin + a_chunk[i] * 8;
+      if (!a_ok[i]) cy_[i] = -(1 << 28);   // never in bounds
     }
   }
   int w_row[WR], w_chunk[WR];
@@ -166,36 +176,63 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
     }
     w_row[i] = gr;
   }
+  long long w_off[WR];
+#pragma unroll
+  for (int i = 0; i < WR; ++i) w_off[i] = (long long)(w_row[i] < 0 ? 0 : w_row[i]) * ldw + w_chunk[i] * 8;
   const int Hv = p.upsample ? 2 * p.IH : p.IH;
   const int Wv = p.upsample ? 2 * p.IW : p.IW;
+  const bool kfull = (p.K % BK) == 0;     // no k bound checks needed
+
+  // wave-uniform conv tap state for CONV >= 2 (Cin % 64 == 0: a k-tile is 64 channels of one
+  // tap), advanced incrementally as the k-tiles are staged in order
+  int t_ci = 0, t_kx = 0, t_ky = 0;
+  auto tap_init = [&](int kt) {
+    const int k0 = kt * BK;
+    const int tap = k0 / p.Cin;
+    t_ci = k0 - tap * p.Cin;
+    t_ky = tap / p.ksize;
+    t_kx = tap - t_ky * p.ksize;
+  };
+  auto tap_next = [&]() {
+    t_ci += BK;
+    if (t_ci == p.Cin) {
+      t_ci = 0;
+      if (++t_kx == p.ksize) { t_kx = 0; ++t_ky; }
+    }
+  };
 
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * BK;
+    const bool kin = kfull || (k0 + BK <= p.K);   // whole tile inside K (uniform)
     uint4* As = smem + buf * TILE;
     uint4* Ws = As + BM * 8;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const int k = k0 + a_chunk[i] * 8;
       const void* src = zp;
       if constexpr (CONV == 0) {
-        if (a_row[i] < p.M && k < p.K) src = A + (long long)a_row[i] * p.lda + k;
-      } else {
-        if (a_row[i] < p.M && k < p.K) {
-          int tap, ci;
-          if constexpr (CONV == 2) {   // Cin % 64 == 0: one tap per k-tile (uniform)
-            tap = k0 / p.Cin;
-            ci = k - tap * p.Cin;
-          } else {
-            tap = k / p.Cin;
-            ci = k - tap * p.Cin;
-          }
+        if (a_ok[i] && (kin || k0 + a_chunk[i] * 8 < p.K)) src = A + a_off[i] + k0;
+      } else if constexpr (CONV == 1) {            // general (Cin % 8): per-lane tap decode
+        const int k = k0 + a_chunk[i] * 8;
+        if (k < p.K) {
+          const int tap = k / p.Cin;
+          const int ci = k - tap * p.Cin;
           const int ky = tap / p.ksize;
           const int kx = tap - ky * p.ksize;
           int iy = cy_[i] + ky, ix = cx_[i] + kx;
-          if (iy >= 0 && iy < Hv && ix >= 0 && ix < Wv) {
+          if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) {
             if (p.upsample) { iy >>= 1; ix >>= 1; }
-            src = A + (((long long)cb_[i] * p.IH + iy) * p.IW + ix) * p.Cin + ci;
+            src = A + (((long long)cbh_[i] + iy) * p.IW + ix) * p.Cin + ci;
           }
+        }
+      } else if constexpr (CONV == 2) {            // Cin % 64, no upsample: linear tap offset
+        const int iy = cy_[i] + t_ky, ix = cx_[i] + t_kx;
+        const long long toff = ((long long)t_ky * p.IW + t_kx) * p.Cin + t_ci;   // uniform
+        if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) src = A + a_off[i] + toff;
+      } else {                                     // CONV == 3: Cin % 64 with fused 2x upsample
+        int iy = cy_[i] + t_ky, ix = cx_[i] + t_kx;
+        if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) {
+          iy >>= 1; ix >>= 1;
+          src = A + (((long long)cbh_[i] + iy) * p.IW + ix) * p.Cin + t_ci + a_chunk[i] * 8;
         }
       }
       glds16(src, As + (32 * i + 8 * wave) * 8);
@@ -203,11 +240,11 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
       if (32 * i + 8 * wave < BN) {          // wave-uniform
-        const int k = k0 + w_chunk[i] * 8;
-        const void* src = (w_row[i] >= 0 && k < p.K) ? (const void*)(W + (long long)w_row[i] * ldw + k) : zp;
+        const void* src = (w_row[i] >= 0 && (kin || k0 + w_chunk[i] * 8 < p.K)) ? (const void*)(W + w_off[i] + k0) : zp;
         glds16(src, Ws + (32 * i + 8 * wave) * 8);
       }
     }
+    if constexpr (CONV >= 2) tap_next();
   };
 
   f32x4_t acc[TI][TJ];
@@ -248,6 +285,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
   const int per = (nk_all + gridDim.y - 1) / gridDim.y;
   const int kt0 = blockIdx.y * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if constexpr (CONV >= 2) tap_init(kt0);
 
   if constexpr (STAGES == 2) {
     if (nk > 0) stage(kt0, 0);
@@ -402,44 +440,76 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32>
 void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
+  // STAGES=3 (counted vmcnt, one block/CU) measured 1.3-1.7x SLOWER than 2 stages at 2
+  // blocks/CU on every SD shape (profiles/r1_ops_stages_ab.txt); define CASSMANTLE_GEMM_3STAGE
+  // to compile it for experiments.
+#ifdef CASSMANTLE_GEMM_3STAGE
   if constexpr (BN % 32 == 0) {
     if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3>(p, ws, s);
   }
+#endif
   launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2>(p, ws, s);
 }
 
+// Tile menu (all 4 waves, 2 blocks per CU by LDS):
+//   0: 128x128 (2x2)   1: 128x160 (2x2, wave 80x64)   2: 256x64 (4x1)   3: 128x64 (2x2)   4: 256x16 (4x1)
+struct TileCfg { int BM, BN; float eff; };
+constexpr TileCfg kTiles[5] = {{128, 128, 1.00f}, {128, 160, 1.02f}, {256, 64, 0.95f}, {128, 64, 0.80f},
+                               {256, 16, 0.25f}};
+constexpr int kSlots = 512;   // resident blocks: 256 CUs x 2
+
 template <int CONV, bool OUTF32>
-void launch_shape(const GemmArgs& p, float* ws, hipStream_t s) {
-  if (p.N <= 16) launch_st<256, 16, 4, 1, CONV, false, OUTF32>(p, ws, s);
-  else if (p.N % 128 != 0 && p.N % 64 == 0) launch_st<256, 64, 4, 1, CONV, false, OUTF32>(p, ws, s);
-  else launch_st<128, 128, 2, 2, CONV, false, OUTF32>(p, ws, s);
+void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
+  switch (p.cfg) {
+    case 1: launch_st<128, 160, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
+    case 2: launch_st<256, 64, 4, 1, CONV, false, OUTF32>(p, ws, s); break;
+    case 3: launch_st<128, 64, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
+    case 4: launch_st<256, 16, 4, 1, CONV, false, OUTF32>(p, ws, s); break;
+    default: launch_st<128, 128, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
+  }
 }
 
 template <int CONV>
 void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
   if (p.act == ACT_GEGLU) launch_st<128, 128, 2, 2, CONV, true, false>(p, ws, s);
-  else if (p.out_f32) launch_shape<CONV, true>(p, ws, s);
-  else launch_shape<CONV, false>(p, ws, s);
+  else if (p.out_f32) launch_cfg<CONV, true>(p, ws, s);
+  else launch_cfg<CONV, false>(p, ws, s);
 }
 
 }  // namespace
 
-int gemm_plan_split(const GemmArgs& p) {
-  // split-K only for grids that cannot fill the chip and have a long K loop; mirrors the
-  // tile choice of launch_shape (GEGLU / batched / ragged shapes never split)
-  if (p.batch != 1 || p.act == ACT_GEGLU || p.N % 4 != 0 || p.K % 8 != 0) return 1;
-  if (p.conv && p.Cin % 8 != 0) return 1;
-  const bool mid = (p.N > 16) && (p.N % 128 != 0 && p.N % 64 == 0);
-  const int BM = (p.N <= 16 || mid) ? 256 : 128;
-  const int BN = p.N <= 16 ? 16 : (mid ? 64 : 128);
-  const long long blocks = (long long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+// Choose tile config + split-K by an occupancy-round cost model: the kernel is latency-bound
+// per k-tile, so time ~ rounds(blocks / 512) x k-tiles-per-block x tile-cost; split-K adds a
+// reduction pass over split x M x N fp32.  Wave quantisation (e.g. 640 blocks = 1.25 rounds)
+// was the single largest loss on the SD shapes (M = 32768 / 8192 / 2048 / 512).
+GemmPlan gemm_plan(const GemmArgs& p) {
+  GemmPlan best{0, 1};
+  if (p.act == ACT_GEGLU) return best;
   const int nk = (p.K + BK - 1) / BK;
-  if (blocks >= 256 || nk < 16) return 1;
-  int split = (int)((512 + blocks - 1) / blocks);
-  split = min(split, nk / 4);
-  split = min(split, GEMM_MAX_SPLIT);
-  return split < 2 ? 1 : split;
+  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0;
+  double best_t = 1e30;
+  for (int c = 0; c < 5; ++c) {
+    const TileCfg& tc = kTiles[c];
+    if (c == 4 && p.N > 16) continue;
+    if (c != 4 && p.N <= 16) continue;
+    const long long tiles = (long long)((p.N + tc.BN - 1) / tc.BN) * ((p.M + tc.BM - 1) / tc.BM) * p.batch;
+    const double waste = (double)tc.BN * ((p.N + tc.BN - 1) / tc.BN) / p.N;   // padded columns
+    for (int split = 1; split <= GEMM_MAX_SPLIT; ++split) {
+      if (split > 1 && (!can_split || nk / split < 4)) break;
+      const long long blocks = tiles * split;
+      const long long rounds = (blocks + kSlots - 1) / kSlots;
+      const int kper = (nk + split - 1) / split;
+      // per-k-tile cost: fixed latency part + size part (normalised to a 128x128 tile)
+      const double tile_cost = (0.55 + 0.45 * (tc.BM * tc.BN) / 16384.0) / tc.eff;
+      double t = rounds * (kper + 2) * tile_cost * (waste > 1.3 ? waste : 1.0);
+      if (split > 1) t += 0.002 * (double)split * p.M * p.N * 4 / 65536.0;   // reduction traffic
+      if (t < best_t - 1e-9) { best_t = t; best = GemmPlan{c, split}; }
+    }
+  }
+  return best;
 }
+
+int gemm_plan_split(const GemmArgs& p) { return gemm_plan(p).split; }
 
 void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
   const bool mfma_ok = (p.K % 8 == 0) && (!p.conv || p.Cin % 8 == 0) &&
@@ -455,6 +525,10 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     return;
   }
   if (!p.conv) launch_tiles<0>(p, ws, s);
-  else if (p.Cin % 64 == 0) launch_tiles<2>(p, ws, s);
-  else launch_tiles<1>(p, ws, s);
+  else if (p.Cin % 64 == 0) {
+    if (p.upsample) launch_tiles<3>(p, ws, s);
+    else launch_tiles<2>(p, ws, s);
+  } else {
+    launch_tiles<1>(p, ws, s);
+  }
 }

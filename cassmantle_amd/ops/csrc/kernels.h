@@ -18,11 +18,14 @@ struct GemmArgs {
   float alpha = 1.f;
   int act = 0;
   int out_f32 = 0;
-  int split = 1;                       // split-K slices (gemm_plan_split)
+  int split = 1;                       // split-K slices (gemm_plan)
+  int cfg = 0;                         // tile config index (gemm_plan)
   // implicit-GEMM convolution (conv != 0)
   int conv = 0, IH = 0, IW = 0, Cin = 0, Ho = 0, Wo = 0, stride = 1, pad = 0, ksize = 1, upsample = 0;
 };
 #define GEMM_MAX_SPLIT 16
+struct GemmPlan { int cfg; int split; };
+GemmPlan gemm_plan(const GemmArgs& p);
 int gemm_plan_split(const GemmArgs& p);
 // ws: fp32 workspace of split * M * N floats when split > 1 (else may be null)
 void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s);
