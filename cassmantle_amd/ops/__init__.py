@@ -177,7 +177,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional
             return o.transpose(1, 2)
         return ref.attention(q, k, v, scale, causal, kv_lens)
     B, Nq, H, _ = q.shape
-    if d > 256:
+    if d > 160:
         return _attention_gemm(q, k, v, scale, causal, kv_lens)
     out = torch.empty((B, Nq, H, d), device=q.device, dtype=q.dtype)
     ext().attention(q, k, v, out, float(scale), int(causal), kv_lens, int(fp8))

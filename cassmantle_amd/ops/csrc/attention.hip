@@ -85,7 +85,13 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
     uint4 v = make_uint4(0, 0, 0, 0);
     int d0 = ks * 16 + 8 * hlf;
     if (q < a.Nq && d0 < d) v = *reinterpret_cast<const uint4*>(Qp + (long long)q * a.q_sn + d0);
-    qf[ks] = as_bf16x8(v);
+    // pre-scale Q by scale*log2(e): S comes out of the MFMA in log2 units, so softmax needs
+    // no per-element multiply
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= a.scale * 1.4426950408889634f;
+    qf[ks] = as_bf16x8(pack8(f));
   }
 
   f32x16_t oacc[NDC];
@@ -93,50 +99,61 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   for (int i = 0; i < NDC; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
-  float m_run = -1e30f, l_run = 0.f;
-  const float c = a.scale * 1.4426950408889634f;
+  float m_run = 0.f, l_run = 0.f;   // m_run: reference max in log2 units (set on the first tile)
   // padded head dims (40 -> 64, 80 -> 96): the first padding column of V carries ones, so the
   // row sum of P comes out of the P.V MFMAs (rescaled with O for free) instead of 32 VALU adds
   // and a cross-half shuffle per tile
   constexpr bool ones = DO > DQK;   // d <= DQK < DO: at least one zero-padded V column
 
+  // staging geometry is tile-invariant: decode (key, chunk) once per thread; per tile only the
+  // uniform key base moves (the first version re-derived it per tile: ~40 VALU per tile)
   uint4 kr[KLD], vr[VLD];
+  int k_key[KLD], v_key[VLD], k_lds[KLD], v_lds[VLD];
+  const uint16_t* k_src[KLD];
+  const uint16_t* v_src[VLD];
+  bool k_use[KLD], v_use[VLD], v_one[VLD];
+#pragma unroll
+  for (int i = 0; i < KLD; ++i) {
+    const int idx = tid + i * THREADS;
+    const int key = idx / G::KCH, ch = idx - key * G::KCH;
+    k_key[i] = key;
+    k_use[i] = key < KT && ch * 8 < d;
+    k_lds[i] = key < KT ? key * G::KSTR + ch * 8 : -1;
+    k_src[i] = Kp + (long long)key * a.k_sn + ch * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < VLD; ++i) {
+    const int idx = tid + i * THREADS;
+    const int key = idx / G::VCH, ch = idx - key * G::VCH;
+    v_key[i] = key;
+    v_use[i] = key < KT && ch * 8 < d;
+    v_one[i] = ones && key < KT && ch * 8 == d;   // V[:, d] = 1.0 -> P.V accumulates the row sum
+    v_lds[i] = key < KT ? key * G::VSTR + ch * 8 : -1;
+    v_src[i] = Vp + (long long)key * a.v_sn + ch * 8;
+  }
   auto gload = [&](int t) {
     const int kbase = t * KT;
+    const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
 #pragma unroll
     for (int i = 0; i < KLD; ++i) {
-      int idx = tid + i * THREADS;
-      int key = idx / G::KCH, ch = idx - key * G::KCH;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (key < KT && kbase + key < nk && ch * 8 < d)
-        v = *reinterpret_cast<const uint4*>(Kp + (long long)(kbase + key) * a.k_sn + ch * 8);
+      if (k_use[i] && kbase + k_key[i] < nk) v = *reinterpret_cast<const uint4*>(k_src[i] + ko);
       kr[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
-      int idx = tid + i * THREADS;
-      int key = idx / G::VCH, ch = idx - key * G::VCH;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (key < KT && kbase + key < nk && ch * 8 < d)
-        v = *reinterpret_cast<const uint4*>(Vp + (long long)(kbase + key) * a.v_sn + ch * 8);
-      else if (ones && ch * 8 == d)
-        v.x = 0x3F80u;   // V[:, d] = 1.0: the P.V MFMA accumulates the softmax row sum in O^T row d
+      uint4 v = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+      if (v_use[i] && kbase + v_key[i] < nk) v = *reinterpret_cast<const uint4*>(v_src[i] + vo);
       vr[i] = v;
     }
   };
   auto lstore = [&]() {
 #pragma unroll
-    for (int i = 0; i < KLD; ++i) {
-      int idx = tid + i * THREADS;
-      int key = idx / G::KCH, ch = idx - key * G::KCH;
-      if (key < KT) *reinterpret_cast<uint4*>(Ks + key * G::KSTR + ch * 8) = kr[i];
-    }
+    for (int i = 0; i < KLD; ++i)
+      if (k_lds[i] >= 0) *reinterpret_cast<uint4*>(Ks + k_lds[i]) = kr[i];
 #pragma unroll
-    for (int i = 0; i < VLD; ++i) {
-      int idx = tid + i * THREADS;
-      int key = idx / G::VCH, ch = idx - key * G::VCH;
-      if (key < KT) *reinterpret_cast<uint4*>(Vs + key * G::VSTR + ch * 8) = vr[i];
-    }
+    for (int i = 0; i < VLD; ++i)
+      if (v_lds[i] >= 0) *reinterpret_cast<uint4*>(Vs + v_lds[i]) = vr[i];
   };
 
   if (ntiles > 0) {
@@ -159,7 +176,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[hf][r] = 0.f;
+      for (int r = 0; r < 16; ++r) sacc[hf][r] = -m_run;   // S - m folded into the MFMA accumulator
       const uint16_t* krow = Ks + (hf * 32 + ql) * G::KSTR + 8 * hlf;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
@@ -182,44 +199,52 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
         }
     }
 
-    // ---- online softmax (lane-local query; partner lane ^32 holds the other 32 keys)
+    // ---- online softmax with a deferred max (lane-local query; lane ^32 holds the other 32
+    // keys).  sacc already holds S - m_run (log2 units).  The reference max only moves when a
+    // query's tile max exceeds it by more than RESCALE_THR (and always on the first tile, whose
+    // m_run = 0 is a placeholder), so p <= 2^THR and the common tile costs one v_exp per score.
+    // At a rescale every quantity still at the old max — O, l and this tile's scores — is
+    // shifted exactly once, before any P of this tile is formed (guide T13 hazard).
+    constexpr float RESCALE_THR = 8.f;
     float mx = -INFINITY;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float mc = m_new * c;
-    float rs = 0.f;
-    if constexpr (ones) {
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[hf][r] = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
-    } else {
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float pv = __builtin_amdgcn_exp2f(fmaf(sacc[hf][r], c, -mc));
-          sacc[hf][r] = pv;
-          rs += pv;
-        }
-      rs += __shfl_xor(rs, 32, 64);
-    }
-    // rescale O only when some query's running max grew (wave-uniform branch; after the
-    // first few tiles the max rarely moves, so the O-wide multiply is usually skipped)
-    if (!__all(m_new == m_run)) {
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+    if (t == 0 || !__all(mx <= RESCALE_THR)) {
+      float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
+      if (!(delta > -1e30f)) delta = 0.f;            // fully masked tile for this query
+      m_run += delta;
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
       l_run *= alpha;
 #pragma unroll
       for (int i = 0; i < NDC; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[hf][r] -= delta;
+    }
+    float rs = 0.f;
+    if constexpr (ones) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[hf][r] = __builtin_amdgcn_exp2f(sacc[hf][r]);
+    } else {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
+          sacc[hf][r] = pv;
+          rs += pv;
+        }
+      rs += __shfl_xor(rs, 32, 64);
     }
     l_run += rs;
-    m_run = m_new;
 
     // ---- P^T fragments (bf16), k-step kk = 2*hf + s uses regs 8s..8s+7 of sacc[hf]
     bf16x8_t pf[4];
@@ -325,7 +350,7 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
       else if (a.d <= 96) launch_nw<96, 96>(a, s);
       else if (a.d <= 128) launch_nw<128, 128>(a, s);
       else if (a.d <= 160) launch_nw<160, 160>(a, s);
-      else launch_nw<256, 256>(a, s);
+      // d > 160 never reaches this kernel: ops.attention routes it to the GEMM path
     }
   }
 }

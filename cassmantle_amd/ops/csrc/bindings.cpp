@@ -146,7 +146,7 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   a.o_sb = out.stride(0); a.o_sn = out.stride(1); a.o_sh = out.stride(2);
   a.B = (int)q.size(0); a.Nq = (int)q.size(1); a.H = (int)q.size(2); a.d = (int)q.size(3);
   a.Nk = (int)k.size(1);
-  TORCH_CHECK(a.d % 8 == 0 && a.d <= 256, "attention: head dim must be a multiple of 8 and <= 256");
+  TORCH_CHECK(a.d % 8 == 0 && a.d <= 160, "attention: head dim must be a multiple of 8 and <= 160");
   for (long long st : {a.q_sb, a.q_sn, a.q_sh, a.k_sb, a.k_sn, a.k_sh, a.v_sb, a.v_sn, a.v_sh})
     TORCH_CHECK(st % 8 == 0, "attention: q/k/v strides must be 16-byte aligned");
   for (long long st : {a.o_sb, a.o_sn, a.o_sh}) TORCH_CHECK(st % 4 == 0, "attention: out strides must be 8-byte aligned");
