@@ -1,0 +1,72 @@
+"""Server entry point.
+
+Single GPU / CPU (reference equivalent of ``uvicorn main:app``)::
+
+    python -m cassmantle_amd.serve --port 8000 [--num_rooms 4] [--image_model sd15] ...
+
+Whole node, rooms data-parallel over the GPUs (one process per GPU, RCCL over xGMI)::
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m cassmantle_amd.serve --num_rooms 8
+
+Rank 0 runs the HTTP/WebSocket front-end and the game state; every rank (0 included) owns the
+rooms ``i mod W`` and generates their images when rank 0's coordinator opens a generation round
+(``parallel.rooms``).  Any ``GameConfig``/``ModelConfig`` field can be passed as ``--field value``
+or ``CASSMANTLE_FIELD`` in the environment.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import sys
+
+WS_PROTOCOL = "cassmantle_amd.api.wsproto:RFC6455Protocol"
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser(add_help=True)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--log-level", default="info")
+    args, rest = ap.parse_known_args(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
+                        format="[%(levelname)s] %(message)s")
+
+    from .config import Config
+    cfg = Config.from_args(rest)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+    import uvicorn
+    from .api.app import create_app
+    from .runtime.factory import build_image_generator, build_service
+
+    if world == 1:
+        app = create_app(build_service(cfg), cfg)
+        uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
+        return 0
+
+    from .parallel import dist as cdist
+    from .parallel.rooms import GenerationCoordinator, RankImageGenerator, RankWorker, RoomSharding
+    ctx = cdist.init_from_env()
+    room_ids = [""] + [str(i) for i in range(1, max(cfg.game.num_rooms, world))]
+    cfg.game.num_rooms = len(room_ids)
+    gen = build_image_generator(cfg, device=str(ctx.device))
+    worker = RankWorker(ctx, gen, RoomSharding(room_ids, ctx.world_size), cfg.game.negative_prompt)
+    if ctx.rank != 0:
+        worker.serve_forever()
+        cdist.shutdown()
+        return 0
+    coord = GenerationCoordinator(worker)
+    svc = build_service(cfg, image_gen_for_room=lambda rid: RankImageGenerator(coord, rid), room_ids=room_ids)
+    app = create_app(svc, cfg)
+    try:
+        uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
+    finally:
+        coord.close()
+        cdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
