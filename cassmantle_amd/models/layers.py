@@ -115,10 +115,17 @@ class CrossAttention(nn.Module):
         self.to_kv = Linear(ctx_dim, 2 * dim, bias=False, gen=gen, dtype=dtype)
         self.to_out = Linear(dim, dim, bias=True, gen=gen, dtype=dtype)
 
+    _kv = None   # view into the UNet's batched context-K/V buffer (set by UNet.set_context)
+
     def forward(self, x, ctx, residual=None, fp8=False):
         B, N, C = x.shape
         q = self.to_q(x).view(B, N, self.heads, self.head_dim)
-        kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, self.heads, self.head_dim)
+        if self._kv is not None and self._kv.shape[0] == B:
+            # the text context is constant over the denoise loop: K/V of every cross-attention
+            # layer come from ONE GEMM per generation (strided views, no copies)
+            kv = self._kv.view(B, self._kv.shape[1], 2, self.heads, self.head_dim)
+        else:
+            kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, self.heads, self.head_dim)
         o = ops.attention(q, kv[:, :, 0], kv[:, :, 1], fp8=fp8)
         return self.to_out(o.reshape(B, N, C), residual=residual)
 

@@ -70,9 +70,12 @@ class ResnetBlock(nn.Module):
         self.conv2 = Conv2d(cout, cout, 3, gen=gen, dtype=dtype)
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0, gen=gen, dtype=dtype) if cin != cout else None
 
-    def forward(self, x, temb_silu):
+    def forward(self, x, temb_silu, tb_all=None):
         h = self.norm1(x, silu=True)
-        tb = self.time_emb_proj(temb_silu)                       # [B, cout]
+        if tb_all is not None:                                   # slice of the UNet-wide batched GEMM
+            tb = tb_all[:, self._tb_off:self._tb_off + self.time_emb_proj.fout]
+        else:
+            tb = self.time_emb_proj(temb_silu)                   # [B, cout]
         h = self.conv1(h, chan_bias=tb)                          # time-emb add fused in epilogue
         h = self.norm2(h, silu=True)
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
@@ -199,28 +202,81 @@ class UNet(nn.Module):
             emb = self.add_linear_2(self.add_linear_1(a_in, act="silu"), residual=emb)
         return _silu(emb)
 
+    # ------------------------------------------------------------------ fused projections
+    def resnets(self) -> List[ResnetBlock]:
+        return [m for m in self.modules() if isinstance(m, ResnetBlock)]
+
+    def cross_attns(self) -> List[CrossAttention]:
+        return [m for m in self.modules() if isinstance(m, CrossAttention)]
+
+    def fuse_projections(self) -> None:
+        """Concatenate every ResNet's time-embedding projection into ONE [sum Cout, 1280] GEMM
+        (22 launch-bound M=B GEMMs per step -> 1) and every cross-attention's context K/V
+        projection into ONE [sum 2C, D_ctx] GEMM (run once per generation by
+        :meth:`set_context`).  Call again after loading weights."""
+        rs = self.resnets()
+        off = 0
+        for r in rs:
+            r._tb_off = off
+            off += r.time_emb_proj.fout
+        # non-persistent buffers: follow .to(device) and stay out of state_dict()
+        self.register_buffer("_tb_w", torch.cat([r.time_emb_proj.weight for r in rs], 0).contiguous(), persistent=False)
+        self.register_buffer("_tb_b", torch.cat([r.time_emb_proj.bias for r in rs], 0).contiguous(), persistent=False)
+        ca = self.cross_attns()
+        off = 0
+        for m in ca:
+            m._kv_off = off
+            off += m.to_kv.fout
+        self.register_buffer("_kv_w", torch.cat([m.to_kv.weight for m in ca], 0).contiguous() if ca else None,
+                             persistent=False)
+        self._kv_bufs: dict = {}
+        self._fused = True
+
+    def set_context(self, ctx: Optional[torch.Tensor]) -> None:
+        """Precompute all cross-attention K/V for a (constant) text context.  Buffers are kept
+        per shape and refilled in place, so a captured denoise graph sees the new context."""
+        if not getattr(self, "_fused", False):
+            self.fuse_projections()
+        ca = self.cross_attns()
+        if ctx is None or self._kv_w is None:
+            for m in ca:
+                m._kv = None
+            return
+        kv = ops.linear(ctx, self._kv_w)                            # [B, L, sum 2C]
+        key = tuple(kv.shape)
+        buf = self._kv_bufs.get(key)
+        if buf is None:
+            self._kv_bufs[key] = buf = kv
+        else:
+            buf.copy_(kv)
+        for m in ca:
+            m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
+
     def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor,
                 added: Optional[dict] = None, fp8: bool = False) -> torch.Tensor:
         """x [B, H, W, 4] NHWC, t [B] (float), ctx [B, 77, D] -> eps [B, H, W, 4]."""
+        if not getattr(self, "_fused", False):
+            self.fuse_projections()
         temb = self.time_embed(t, added)
+        tb = ops.linear(temb, self._tb_w, self._tb_b)               # all ResNets' time biases
         h = self.conv_in(x)
         skips = [h]
         for blk in self.down:
             for j, res in enumerate(blk.resnets):
-                h = res(h, temb)
+                h = res(h, temb, tb)
                 if len(blk.attentions):
                     h = blk.attentions[j](h, ctx, fp8)
                 skips.append(h)
             if blk.downsampler is not None:
                 h = blk.downsampler(h)
                 skips.append(h)
-        h = self.mid_res1(h, temb)
+        h = self.mid_res1(h, temb, tb)
         h = self.mid_attn(h, ctx, fp8)
-        h = self.mid_res2(h, temb)
+        h = self.mid_res2(h, temb, tb)
         for blk in self.up:
             for j, res in enumerate(blk.resnets):
                 h = torch.cat([h, skips.pop()], dim=-1)
-                h = res(h, temb)
+                h = res(h, temb, tb)
                 if len(blk.attentions):
                     h = blk.attentions[j](h, ctx, fp8)
             if blk.upsampler is not None:

@@ -73,7 +73,13 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   GemmArgs p;
   p.conv = 1;
   p.A = bptr(x); p.W = bptr(w); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
-  p.chan_bias = opt_bptr(chan_bias);
+  if (chan_bias.has_value() && chan_bias->defined()) {
+    CHECK_DEV(*chan_bias);
+    CHECK_BF16(*chan_bias);
+    TORCH_CHECK(chan_bias->dim() == 2 && chan_bias->stride(1) == 1, "conv2d: chan_bias must be [B, Cout] rows");
+    p.chan_bias = bptr(*chan_bias);
+    p.ldcb = (int)chan_bias->stride(0);
+  }
   p.IH = (int)x.size(1); p.IW = (int)x.size(2); p.Cin = (int)x.size(3);
   p.ksize = (int)w.size(1);
   TORCH_CHECK(w.size(2) == p.ksize && w.size(3) == p.Cin, "conv2d: weight must be [Cout,k,k,Cin]");
@@ -86,7 +92,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   p.stride = (int)stride; p.pad = (int)pad; p.upsample = (int)upsample;
   if (residual.has_value() && residual->defined()) TORCH_CHECK(residual->numel() == out.numel(), "conv2d: residual shape");
   if (chan_bias.has_value() && chan_bias->defined())
-    TORCH_CHECK(chan_bias->numel() == x.size(0) * p.N, "conv2d: chan_bias must be [B, Cout]");
+    TORCH_CHECK(chan_bias->size(0) == x.size(0) && chan_bias->size(1) == p.N, "conv2d: chan_bias must be [B, Cout]");
   p.C = out.data_ptr();
   run_gemm(p, out);
 }

@@ -60,12 +60,13 @@ template <bool OUTF32>
 CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   const int hw = p.Ho * p.Wo;
   const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
-  const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0);
+  const long long cbs = p.ldcb ? p.ldcb : p.N;
+  const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (cbs % 4 == 0);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
   if (full) {
     if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
-    if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * p.N + n));
+    if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
     if (p.act != ACT_NONE) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
@@ -84,7 +85,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
       if (n + r >= p.N) break;
       float v = o[r];
       if (p.bias) v += bf2f(p.bias[n + r]);
-      if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * p.N + n + r]);
+      if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * cbs + n + r]);
       v = apply_act(v, p.act);
       if (p.residual) v += bf2f(p.residual[(long long)m * p.ldc + n + r]);
       if constexpr (OUTF32)
@@ -394,7 +395,7 @@ __global__ void gemm_simt_kernel(GemmArgs p) {
   }
   float o = s * p.alpha;
   if (p.bias) o += bf2f(p.bias[n]);
-  if (p.chan_bias) o += bf2f(p.chan_bias[(long long)(m / (p.Ho * p.Wo)) * p.N + n]);
+  if (p.chan_bias) o += bf2f(p.chan_bias[(long long)(m / (p.Ho * p.Wo)) * (p.ldcb ? p.ldcb : p.N) + n]);
   o = apply_act(o, p.act);
   if (p.residual) o += bf2f(p.residual[(long long)m * p.ldc + n]);
   if (p.out_f32)
@@ -486,7 +487,8 @@ GemmPlan gemm_plan(const GemmArgs& p) {
   GemmPlan best{0, 1};
   if (p.act == ACT_GEGLU) return best;
   const int nk = (p.K + BK - 1) / BK;
-  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0;
+  // tiny-M GEMMs (time-embedding / pooled projections) are launch-bound: never split them
+  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M >= 128;
   double best_t = 1e30;
   for (int c = 0; c < 5; ++c) {
     const TileCfg& tc = kTiles[c];

@@ -10,6 +10,7 @@ struct GemmArgs {
   const uint16_t* bias = nullptr;       // [Nw] (geglu: [2N])
   const uint16_t* residual = nullptr;   // [M][ldc]
   const uint16_t* chan_bias = nullptr;  // [B][N] per-image bias (ResNet time embedding)
+  int ldcb = 0;                         // chan_bias row stride (0 -> N): slices of one batched GEMM
   void* C = nullptr;                    // [batch][M][ldc] bf16 or f32
   int M = 0, N = 0, K = 0, Nw = 0;
   int lda = 0, ldc = 0, ldw = 0;      // ldw = W row stride (0 -> K)

@@ -164,6 +164,9 @@ class StableDiffusion:
                 added: Optional[dict] = None) -> torch.Tensor:
         B = latents.shape[0]
         st = self._state(B, ctx, plan, added)
+        # cross-attention K/V of the (loop-invariant) text context: one GEMM per generation,
+        # written into per-shape buffers that the captured step graph reads
+        self.unet.set_context(ctx)
         if self.use_graphs and st.graph is None:
             st.load(latents, ctx, added)
             self._capture(st)
