@@ -308,7 +308,81 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
     }
   }
 
-  // ---- epilogue
+  // ---- LDS-staged epilogue (bf16 output, no split): the MFMA layout gives each lane 4
+  // consecutive columns of one row (8-byte stores, 32 B per row per instruction); instead the
+  // tile is written to LDS (bias / time-bias / activation applied in registers) and streamed out
+  // as full rows of 16-byte stores, residual added in the same coalesced pass.
+  if constexpr (!OUTF32) {
+    constexpr int OBN = GEGLU ? BN / 2 : BN;   // output columns of this tile
+    constexpr int OST = OBN + 8;               // LDS row stride (elements): 16-B pad
+    const long long cbs = p.ldcb ? p.ldcb : p.N;
+    const bool lds_ok = gridDim.y == 1 && (p.N % 8 == 0) && (p.ldc % 8 == 0) && (cbs % 4 == 0);
+    if (lds_ok) {
+      __syncthreads();                        // every wave is done with the staging buffers
+      uint16_t* T = reinterpret_cast<uint16_t*>(smem);
+      const int hw = p.Ho * p.Wo;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int ml = wm * (BM / WM) + 16 * j + fr;
+        const int m = m0 + ml;
+        const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
+        if constexpr (GEGLU) {
+#pragma unroll
+          for (int pi = 0; pi < TI / 2; ++pi) {
+            const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;
+            const int n = n0 + nl;
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
+              if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
+              o[r] = h * gelu_f(g);
+            }
+            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) {
+            const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
+            const int n = n0 + nl;
+            float o[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
+                          acc[i][j][3] * p.alpha};
+            if (n < p.N && m < p.M) {
+              if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
+              if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
+              if (p.act != ACT_NONE) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
+              }
+            }
+            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+        }
+      }
+      __syncthreads();
+      constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
+      uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
+      for (int c = tid; c < BM * CPR; c += THREADS) {
+        const int row = c / CPR, c8 = c - row * CPR;
+        const int m = m0 + row, n = n0 + c8 * 8;
+        if (m >= p.M || n >= p.N) continue;
+        uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
+        if (p.residual) {
+          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + (long long)m * p.ldc + n);
+          float a[8], b[8];
+          unpack8(v, a);
+          unpack8(rv, b);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += b[e];
+          v = pack8(a);
+        }
+        *reinterpret_cast<uint4*>(Cb + (long long)m * p.ldc + n) = v;
+      }
+      return;
+    }
+  }
+
+  // ---- direct epilogue (fp32 outputs, split-K partial slabs, ragged N)
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int m = m0 + wm * (BM / WM) + 16 * j + fr;
@@ -503,8 +577,10 @@ GemmPlan gemm_plan(const GemmArgs& p) {
       const int kper = (nk + split - 1) / split;
       // per-k-tile cost: fixed latency part + size part (normalised to a 128x128 tile)
       const double tile_cost = (0.55 + 0.45 * (tc.BM * tc.BN) / 16384.0) / tc.eff;
-      double t = rounds * (kper + 2) * tile_cost * (waste > 1.3 ? waste : 1.0);
-      if (split > 1) t += 0.002 * (double)split * p.M * p.N * 4 / 65536.0;   // reduction traffic
+      // calibrated on MI355X: ~1.8 us per 128x128x64 k-tile per occupancy round (2 blocks/CU)
+      double t = 1.8 * rounds * (kper + 2) * tile_cost * (waste > 1.3 ? waste : 1.0);
+      // split-K: slab write + read at ~3 TB/s plus the extra reduce launch (~6 us in a graph)
+      if (split > 1) t += 6.0 + 2.0 * (double)split * p.M * p.N * 4 / 3.0e6;
       if (t < best_t - 1e-9) { best_t = t; best = GemmPlan{c, split}; }
     }
   }
