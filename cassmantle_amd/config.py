@@ -89,7 +89,16 @@ class ModelConfig:
     seed: int = 0
     scorer: str = "minilm"               # minilm | wordvec
     scorer_batch_window_ms: float = 1.0   # micro-batch window for streaming guess scoring
-    prompt_generator: str = "synthetic"   # synthetic | lm
+    prompt_generator: str = "synthetic"   # synthetic | lm | remote
+    lm_model: str = "tiny-lm"             # tiny-lm | mistral-7b (models/lm.py)
+    lm_weights: Optional[str] = None      # HF-layout safetensors dir/file for the LM
+    lm_tokenizer: Optional[str] = None    # sentencepiece model (else byte-level tokenizer)
+    # --- remote generation (reference parity: HF inference endpoints, src/backend.py:24-25) ---
+    remote_prompt_url: Optional[str] = None
+    remote_image_url: Optional[str] = None
+    remote_token: Optional[str] = None    # bearer token (reference reads it from a file)
+    remote_timeout_s: float = 60.0        # src/backend.py:99,175
+    remote_retry_s: float = 10.0          # backoff unit: sleep 10*(retry+1) on 503 (src/utils.py:55-57)
 
 
 @dataclass

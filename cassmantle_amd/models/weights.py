@@ -154,6 +154,63 @@ def load_state(model: nn.Module, sd: Dict[str, torch.Tensor], kind: str, strict:
     return missing
 
 
+def load_causal_lm(model: nn.Module, sd: Dict[str, torch.Tensor]) -> List[str]:
+    """HF Llama/Mistral layout (``model.layers.i.self_attn.q_proj.weight`` ...) ->
+    :class:`~cassmantle_amd.models.lm.CausalLM`: q/k/v fused into ``qkv``, ``[up; gate]`` fused
+    into ``gate_up`` (SwiGLU epilogue order).  Returns missing names."""
+    missing: List[str] = []
+
+    def get(name):
+        t = sd.get(name)
+        if t is None:
+            missing.append(name)
+        return t
+
+    with torch.no_grad():
+        def put(dst, t):
+            if t is not None:
+                if tuple(t.shape) != tuple(dst.shape):
+                    raise ValueError(f"checkpoint {tuple(t.shape)} vs model {tuple(dst.shape)}")
+                dst.copy_(t.to(dst.dtype))
+
+        put(model.embed, get("model.embed_tokens.weight"))
+        put(model.norm, get("model.norm.weight"))
+        put(model.lm_head, sd.get("lm_head.weight", sd.get("model.embed_tokens.weight")))
+        for i, blk in enumerate(model.blocks):
+            p = f"model.layers.{i}."
+            put(blk.attn_norm, get(p + "input_layernorm.weight"))
+            put(blk.mlp_norm, get(p + "post_attention_layernorm.weight"))
+            q, k, v = (get(p + f"self_attn.{n}_proj.weight") for n in ("q", "k", "v"))
+            if q is not None and k is not None and v is not None:
+                put(blk.qkv, torch.cat([q, k, v], 0))
+            put(blk.o, get(p + "self_attn.o_proj.weight"))
+            up, gate = get(p + "mlp.up_proj.weight"), get(p + "mlp.gate_proj.weight")
+            if up is not None and gate is not None:
+                put(blk.gate_up, torch.cat([up, gate], 0))
+            put(blk.down, get(p + "mlp.down_proj.weight"))
+    return missing
+
+
+def export_causal_lm(model: nn.Module) -> Dict[str, torch.Tensor]:
+    """Inverse of :func:`load_causal_lm` (HF names, split projections)."""
+    c = model.c
+    hd = c.head_dim
+    out = {"model.embed_tokens.weight": model.embed, "model.norm.weight": model.norm,
+           "lm_head.weight": model.lm_head}
+    for i, blk in enumerate(model.blocks):
+        p = f"model.layers.{i}."
+        out[p + "input_layernorm.weight"] = blk.attn_norm
+        out[p + "post_attention_layernorm.weight"] = blk.mlp_norm
+        q, k, v = torch.split(blk.qkv, [c.heads * hd, c.kv_heads * hd, c.kv_heads * hd], 0)
+        out[p + "self_attn.q_proj.weight"], out[p + "self_attn.k_proj.weight"] = q, k
+        out[p + "self_attn.v_proj.weight"] = v
+        out[p + "self_attn.o_proj.weight"] = blk.o
+        up, gate = blk.gate_up.chunk(2, 0)
+        out[p + "mlp.up_proj.weight"], out[p + "mlp.gate_proj.weight"] = up, gate
+        out[p + "mlp.down_proj.weight"] = blk.down
+    return {k: v.detach().cpu().contiguous() for k, v in out.items()}
+
+
 def read_safetensors(path: str) -> Dict[str, torch.Tensor]:
     from safetensors.torch import load_file
     if os.path.isdir(path):

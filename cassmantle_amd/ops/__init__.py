@@ -45,7 +45,7 @@ def _use_hip(t: torch.Tensor) -> bool:
     return True
 
 
-_ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5}
+_ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5, "swiglu": 6}
 
 
 # ----------------------------------------------------------------------------- GEMM (K6)
@@ -60,7 +60,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     x2 = x.reshape(-1, K)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
-    N = w.shape[0] // 2 if act == "geglu" else w.shape[0]
+    N = w.shape[0] // 2 if act in ("geglu", "swiglu") else w.shape[0]
     out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
     r2 = residual.reshape(-1, N) if residual is not None else None
     ext().gemm(x2, w, bias, r2, out, _ACT[act])
@@ -73,6 +73,9 @@ def _torch_linear(x, w, bias, residual, act):
     if act == "geglu":
         h, g = y.chunk(2, dim=-1)
         y = h * F.gelu(g)
+    elif act == "swiglu":
+        h, g = y.chunk(2, dim=-1)
+        y = h * F.silu(g)
     elif act == "gelu":
         y = F.gelu(y)
     elif act == "gelu_tanh":
@@ -157,6 +160,38 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    if not _use_hip(x):
+        return ref.rms_norm(x, weight, eps)
+    out = torch.empty_like(x)
+    ext().rms_norm(x.contiguous(), weight, out, float(eps))
+    return out
+
+
+# ----------------------------------------------------------------------------- causal-LM decode path
+def rope_kv(qkv: torch.Tensor, pos0: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
+            v_cache: torch.Tensor, heads: int, kv_heads: int, theta: float) -> None:
+    """Fused rotary embedding + KV-cache append.  qkv [B, T, (H+2Hk)*d] (fused projection),
+    pos0 [B] int32 device positions of token 0 -> q_out [B, T, H, d] rotated; rotated K and V
+    written to the caches [B, L, Hk, d] at pos0[b] + t.  In place."""
+    if not _use_hip(qkv):
+        ref.rope_kv(qkv, pos0, q_out, k_cache, v_cache, heads, kv_heads, theta)
+        return
+    ext().rope_kv(qkv, pos0, q_out, k_cache, v_cache, int(heads), int(kv_heads), float(theta))
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
+                     scale: Optional[float] = None) -> torch.Tensor:
+    """One query token per sequence.  q [B, H, d]; caches [B, L, Hk, d]; lens [B] int32 (device)
+    valid keys per sequence.  Split-KV GQA kernel; graph-capturable (lens stays on device)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if not _use_hip(q):
+        return ref.decode_attention(q, k_cache, v_cache, lens, scale)
+    out = torch.empty_like(q)
+    ext().decode_attention(q, k_cache, v_cache, lens, out, float(scale))
+    return out
+
+
 # ----------------------------------------------------------------------------- attention (K1/K2/K3)
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,
               causal: bool = False, kv_lens: Optional[torch.Tensor] = None,
@@ -168,6 +203,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional
     if not _use_hip(q):
         if q.device.type == "cuda":
             import torch.nn.functional as F
+            if k.shape[2] != q.shape[2]:
+                g = q.shape[2] // k.shape[2]
+                k, v = k.repeat_interleave(g, dim=2), v.repeat_interleave(g, dim=2)
             mask = None
             if kv_lens is not None:
                 ar = torch.arange(k.shape[1], device=q.device)

@@ -74,8 +74,9 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   if (a.causal) ntiles = min(ntiles, (qb * QB + QB + KT - 1) / KT);
 
   const uint16_t* Qp = a.q + (long long)b * a.q_sb + (long long)h * a.q_sh;
-  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)h * a.k_sh;
-  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)h * a.v_sh;
+  const int hk = a.group > 1 ? h / a.group : h;   // grouped-query attention (LM prefill)
+  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)hk * a.k_sh;
+  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)hk * a.v_sh;
   const int d = a.d;
 
   // Q^T fragments: lane holds Q[q][ks*16 + 8*hlf .. +7]

@@ -50,8 +50,8 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   p.lda = (int)x.stride(0); p.ldc = p.N; p.act = (int)act;
   TORCH_CHECK(w.size(1) == p.K, "gemm: K mismatch");
   TORCH_CHECK(out.size(0) == p.M, "gemm: M mismatch");
-  if (act == 4) {
-    TORCH_CHECK(p.Nw == 2 * p.N && p.K % 8 == 0 && p.N % 4 == 0, "geglu: W must be [2N,K], K%8==0, N%4==0");
+  if (act == 4 || act == 6) {
+    TORCH_CHECK(p.Nw == 2 * p.N && p.K % 8 == 0 && p.N % 4 == 0, "geglu/swiglu: W must be [2N,K], K%8==0, N%4==0");
   } else {
     TORCH_CHECK(p.Nw == p.N, "gemm: N mismatch");
   }
@@ -153,6 +153,8 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   a.B = (int)q.size(0); a.Nq = (int)q.size(1); a.H = (int)q.size(2); a.d = (int)q.size(3);
   a.Nk = (int)k.size(1);
   TORCH_CHECK(a.d % 8 == 0 && a.d <= 160, "attention: head dim must be a multiple of 8 and <= 160");
+  TORCH_CHECK(k.size(2) == v.size(2) && a.H % k.size(2) == 0, "attention: query heads must be a multiple of kv heads");
+  a.group = a.H / (int)k.size(2);
   for (long long st : {a.q_sb, a.q_sn, a.q_sh, a.k_sb, a.k_sn, a.k_sh, a.v_sb, a.v_sn, a.v_sh})
     TORCH_CHECK(st % 8 == 0, "attention: q/k/v strides must be 16-byte aligned");
   for (long long st : {a.o_sb, a.o_sn, a.o_sh}) TORCH_CHECK(st % 4 == 0, "attention: out strides must be 8-byte aligned");
@@ -251,6 +253,58 @@ void softmax_rows(const at::Tensor& S, at::Tensor& P, int64_t causal, const c10:
   launch_softmax_rows(S.data_ptr<float>(), bptr_mut(P), rows, cols, Nq, (int)causal, kl, cur_stream());
 }
 
+void rms_norm(const at::Tensor& x, const at::Tensor& gamma, at::Tensor& out, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(gamma); CHECK_CONTIG(out);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 4096 && gamma.numel() == D, "rms_norm: D % 8 == 0, D <= 4096");
+  launch_rms_norm(bptr(x), bptr(gamma), bptr_mut(out), x.numel() / D, D, (float)eps, cur_stream());
+}
+
+// qkv [B, T, (H + 2Hk) * d] -> q_out [B, T, H, d] (rotated), K (rotated) / V into the caches
+// [B, L, Hk, d] at positions pos0[b] + t
+void rope_kv(const at::Tensor& qkv, const at::Tensor& pos0, at::Tensor& q_out, at::Tensor& k_cache,
+             at::Tensor& v_cache, int64_t H, int64_t Hk, double theta) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_BF16(q_out); CHECK_CONTIG(q_out);
+  CHECK_BF16(k_cache); CHECK_CONTIG(k_cache); CHECK_BF16(v_cache); CHECK_CONTIG(v_cache);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.stride(2) == 1, "rope_kv: qkv [B, T, C] with contiguous rows");
+  TORCH_CHECK(pos0.scalar_type() == at::kInt && pos0.is_cuda(), "rope_kv: pos0 int32 on device");
+  RopeArgs a;
+  a.B = (int)qkv.size(0); a.T = (int)qkv.size(1); a.H = (int)H; a.Hk = (int)Hk;
+  a.d = (int)q_out.size(3); a.L = (int)k_cache.size(1);
+  TORCH_CHECK(qkv.size(2) == (H + 2 * Hk) * a.d && a.d % 2 == 0, "rope_kv: qkv width");
+  TORCH_CHECK(qkv.stride(1) * a.T == qkv.stride(0), "rope_kv: qkv tokens must be packed per batch");
+  TORCH_CHECK(k_cache.size(0) == a.B && k_cache.size(2) == Hk && k_cache.size(3) == a.d, "rope_kv: cache shape");
+  a.qkv = bptr(qkv); a.ld = qkv.stride(1); a.pos0 = pos0.data_ptr<int>();
+  a.q_out = bptr_mut(q_out); a.k_cache = bptr_mut(k_cache); a.v_cache = bptr_mut(v_cache);
+  a.log2_theta = (float)std::log2(theta);
+  launch_rope_kv(a, cur_stream());
+}
+
+// one query token per sequence: q [B, H, d], caches [B, L, Hk, d], lens [B] -> out [B, H, d]
+void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                      const at::Tensor& lens, at::Tensor& out, double scale) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
+  CHECK_BF16(out);
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.is_cuda(), "decode_attention: lens int32 on device");
+  DecodeArgs a;
+  a.B = (int)q.size(0); a.H = (int)q.size(1); a.d = (int)q.size(2);
+  a.L = (int)k_cache.size(1); a.Hk = (int)k_cache.size(2);
+  TORCH_CHECK(q.stride(2) == 1 && q.stride(1) == a.d && out.stride(2) == 1 && out.stride(1) == a.d,
+              "decode_attention: heads must be packed");
+  TORCH_CHECK(a.d == 64 || a.d == 128, "decode_attention: head dim 64 or 128");
+  TORCH_CHECK(a.H % a.Hk == 0 && a.H / a.Hk <= 8, "decode_attention: 1..8 query heads per kv head");
+  a.q = bptr(q); a.q_sb = q.stride(0); a.k_cache = bptr(k_cache); a.v_cache = bptr(v_cache);
+  a.lens = lens.data_ptr<int>(); a.o = bptr_mut(out); a.o_sb = out.stride(0); a.scale = (float)scale;
+  const int ns = decode_splits(a.B, a.Hk, a.L);
+  at::Tensor ws;
+  a.ws = nullptr;
+  if (ns > 1) {
+    ws = at::empty({(long long)a.B * a.H * ns * (a.d + 2)}, q.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+  }
+  launch_decode_attention(a, ns, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -271,5 +325,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("latent_step", &latent_step);
   m.def("advance_step", &advance_step);
   m.def("softmax_rows", &softmax_rows);
+  m.def("rms_norm", &rms_norm);
+  m.def("rope_kv", &rope_kv);
+  m.def("decode_attention", &decode_attention);
   m.attr("arch") = "gfx950";
 }

@@ -54,7 +54,12 @@ CM_DEVICE float gelu_tanh_f(float x) {
 CM_DEVICE float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
 
 // activation codes shared with python (ops/__init__.py _ACT)
-enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_QUICK_GELU = 3, ACT_GEGLU = 4, ACT_GELU_TANH = 5 };
+// Gated acts (GEGLU: h*gelu(g), SWIGLU: h*silu(g)) read a [value; gate] weight of 2N rows.
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_QUICK_GELU = 3, ACT_GEGLU = 4, ACT_GELU_TANH = 5,
+           ACT_SWIGLU = 6 };
+
+__host__ __device__ inline bool is_gated(int act) { return act == ACT_GEGLU || act == ACT_SWIGLU; }
+CM_DEVICE float gate_f(float h, float g, int act) { return h * (act == ACT_SWIGLU ? silu_f(g) : gelu_f(g)); }
 
 CM_DEVICE float apply_act(float x, int act) {
   switch (act) {

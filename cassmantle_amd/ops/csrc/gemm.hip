@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
             for (int r = 0; r < 4; ++r) {
               float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
               if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-              o[r] = h * gelu_f(g);
+              o[r] = gate_f(h, g, p.act);
             }
             *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
           }
@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
         for (int r = 0; r < 4; ++r) {
           float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
           if (p.bias) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-          o[r] = h * gelu_f(g);
+          o[r] = gate_f(h, g, p.act);
         }
         uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
         if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
@@ -546,7 +546,7 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
 
 template <int CONV>
 void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
-  if (p.act == ACT_GEGLU) launch_st<128, 128, 2, 2, CONV, true, false>(p, ws, s);
+  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) launch_st<128, 128, 2, 2, CONV, true, false>(p, ws, s);
   else if (p.out_f32) launch_cfg<CONV, true>(p, ws, s);
   else launch_cfg<CONV, false>(p, ws, s);
 }
@@ -559,7 +559,7 @@ void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
 // was the single largest loss on the SD shapes (M = 32768 / 8192 / 2048 / 512).
 GemmPlan gemm_plan(const GemmArgs& p) {
   GemmPlan best{0, 1};
-  if (p.act == ACT_GEGLU) return best;
+  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) return best;
   const int nk = (p.K + BK - 1) / BK;
   // tiny-M GEMMs (time-embedding / pooled projections) are launch-bound: never split them
   const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M >= 128;
@@ -592,8 +592,10 @@ int gemm_plan_split(const GemmArgs& p) { return gemm_plan(p).split; }
 void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
   const bool mfma_ok = (p.K % 8 == 0) && (!p.conv || p.Cin % 8 == 0) &&
                        (p.conv || p.lda % 8 == 0) && (p.ldw % 8 == 0);
+  // skinny M (decode tokens, time-embedding / pooled projections): a weight-streaming GEMV
+  if (launch_gemv(p, s)) return;
   if (!mfma_ok) {
-    if (p.act == ACT_GEGLU) return;  // host side guarantees geglu shapes are MFMA-able
+    if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) return;  // host guarantees gated shapes are MFMA-able
     long long total = (long long)p.M * p.N;
     dim3 grid((unsigned)((total + 255) / 256), 1, p.batch);
     if (p.conv)

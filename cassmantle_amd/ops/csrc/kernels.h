@@ -41,6 +41,7 @@ struct AttnArgs {
   float scale;
   int causal;
   const int* kv_lens;             // [B] or null
+  int group = 1;                  // query heads per K/V head (GQA)
 };
 void launch_attention(const AttnArgs& a, hipStream_t s);
 
@@ -50,6 +51,31 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
 long long group_norm_workspace(int B, long long S, int C);
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        long long rows, int D, float eps, hipStream_t s);
+void launch_rms_norm(const uint16_t* x, const uint16_t* gamma, uint16_t* y, long long rows, int D, float eps,
+                     hipStream_t s);
+
+// decode path (lm.hip)
+bool launch_gemv(const GemmArgs& p, hipStream_t s);   // false -> shape not handled (M > 8, conv, ...)
+struct RopeArgs {
+  const uint16_t* qkv; long long ld;   // [B*T][ld], heads [q | k | v] x d
+  const int* pos0;                     // [B] first position of this chunk (null -> 0)
+  uint16_t* q_out;                     // [B][T][H][d]
+  uint16_t* k_cache; uint16_t* v_cache;   // [B][L][Hk][d]
+  int B, T, H, Hk, d, L;
+  float log2_theta;
+};
+void launch_rope_kv(const RopeArgs& a, hipStream_t s);
+struct DecodeArgs {
+  const uint16_t* q; long long q_sb;   // [B][H][d] (batch stride q_sb)
+  const uint16_t* k_cache; const uint16_t* v_cache;   // [B][L][Hk][d]
+  const int* lens;                     // [B] valid keys (device)
+  uint16_t* o; long long o_sb;         // [B][H][d]
+  float* ws;                           // split partials [B*H][ns][d+2]
+  int B, H, Hk, d, L;
+  float scale;
+};
+int decode_splits(int B, int Hk, int L);
+void launch_decode_attention(const DecodeArgs& a, int ns, hipStream_t s);
 
 // scorer
 void launch_gather_cosine(const void* table, int table_f32, int D, const int* ia, const int* ib,

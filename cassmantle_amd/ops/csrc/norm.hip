@@ -138,8 +138,8 @@ __global__ void gn_apply_kernel(const uint16_t* __restrict__ x, const float* __r
   }
 }
 
-// LayerNorm: one wave per row; D <= 64*8*MAXV
-template <int MAXV>
+// LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): one wave per row; D <= 64*8*MAXV
+template <int MAXV, bool RMS>
 __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gamma,
                           const uint16_t* __restrict__ beta, uint16_t* __restrict__ y,
                           long long rows, int D, float eps) {
@@ -159,7 +159,7 @@ __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __rest
       for (int k = 0; k < 8; ++k) s += f[j][k];
     }
   }
-  const float mean = wave_sum(s) / D;
+  const float mean = RMS ? 0.f : wave_sum(s) / D;
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
@@ -223,12 +223,23 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
   hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, scale, shift, y, S, C, B, silu);
 }
 
-void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
-                       long long rows, int D, float eps, hipStream_t s) {
+template <bool RMS>
+static void launch_ln(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                      long long rows, int D, float eps, hipStream_t s) {
   const int V = D / 8;
   dim3 grid((unsigned)((rows + 3) / 4));
-  if (V <= 64) hipLaunchKernelGGL(ln_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else if (V <= 128) hipLaunchKernelGGL(ln_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else if (V <= 256) hipLaunchKernelGGL(ln_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else hipLaunchKernelGGL(ln_kernel<8>, grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+  if (V <= 64) hipLaunchKernelGGL((ln_kernel<1, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+  else if (V <= 128) hipLaunchKernelGGL((ln_kernel<2, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+  else if (V <= 256) hipLaunchKernelGGL((ln_kernel<4, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+  else hipLaunchKernelGGL((ln_kernel<8, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+}
+
+void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                       long long rows, int D, float eps, hipStream_t s) {
+  launch_ln<false>(x, gamma, beta, y, rows, D, eps, s);
+}
+
+void launch_rms_norm(const uint16_t* x, const uint16_t* gamma, uint16_t* y, long long rows, int D, float eps,
+                     hipStream_t s) {
+  launch_ln<true>(x, gamma, nullptr, y, rows, D, eps, s);
 }

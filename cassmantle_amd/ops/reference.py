@@ -44,6 +44,9 @@ def linear(x, w, bias=None, residual=None, act=None, out_dtype=None):
     if act == "geglu":
         h, g = y.chunk(2, dim=-1)
         y = h * F.gelu(g)
+    elif act == "swiglu":
+        h, g = y.chunk(2, dim=-1)
+        y = h * F.silu(g)
     else:
         y = _act(y, act)
     if residual is not None:
@@ -85,11 +88,56 @@ def layer_norm(x, weight, bias, eps):
     return F.layer_norm(x.float(), (x.shape[-1],), weight.float(), None if bias is None else bias.float(), eps).to(x.dtype)
 
 
+def rms_norm(x, weight, eps):
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()).to(x.dtype)
+
+
+def rope(x, pos, theta):
+    """Rotate-half rotary embedding.  x [B, T, h, d]; pos [B, T] int positions."""
+    d = x.shape[-1]
+    inv = theta ** (-torch.arange(0, d // 2, device=x.device, dtype=torch.float32) * 2.0 / d)
+    ang = pos.float()[..., None] * inv                       # [B, T, d/2]
+    cos, sin = ang.cos()[:, :, None, :], ang.sin()[:, :, None, :]
+    xf = x.float()
+    x0, x1 = xf[..., : d // 2], xf[..., d // 2:]
+    return torch.cat([x0 * cos - x1 * sin, x1 * cos + x0 * sin], dim=-1).to(x.dtype)
+
+
+def rope_kv(qkv, pos0, q_out, k_cache, v_cache, H, Hk, theta):
+    """Reference of the fused RoPE + KV-cache append (in place on q_out / caches)."""
+    B, T, _ = qkv.shape
+    d = q_out.shape[-1]
+    x = qkv.view(B, T, H + 2 * Hk, d)
+    pos = pos0.long()[:, None] + torch.arange(T, device=qkv.device)[None, :]
+    q_out.copy_(rope(x[:, :, :H], pos, theta))
+    kr = rope(x[:, :, H:H + Hk], pos, theta)
+    for b in range(B):
+        p0 = int(pos0[b])
+        n = max(0, min(T, k_cache.shape[1] - p0))
+        k_cache[b, p0:p0 + n] = kr[b, :n]
+        v_cache[b, p0:p0 + n] = x[b, :n, H + Hk:]
+
+
+def decode_attention(q, k_cache, v_cache, lens, scale):
+    """q [B, H, d] one token vs cache [B, L, Hk, d] with lens[b] valid keys -> [B, H, d]."""
+    B, H, d = q.shape
+    out = torch.empty_like(q)
+    for b in range(B):
+        n = int(lens[b])
+        o = attention(q[b:b + 1, None], k_cache[b:b + 1, :n], v_cache[b:b + 1, :n], scale)
+        out[b] = o[0, 0]
+    return out
+
+
 def attention(q, k, v, scale=None, causal=False, kv_lens=None):
     """q [B,Nq,H,d], k/v [B,Nk,H,d] (any strides, last dim contiguous) -> o [B,Nq,H,d].
     ``kv_lens`` [B] int: keys >= len are masked (padding mask)."""
     d = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(d)
+    if k.shape[2] != q.shape[2]:   # grouped-query attention: expand the kv heads
+        g = q.shape[2] // k.shape[2]
+        k, v = k.repeat_interleave(g, dim=2), v.repeat_interleave(g, dim=2)
     qf = q.float().permute(0, 2, 1, 3)
     kf = k.float().permute(0, 2, 1, 3)
     vf = v.float().permute(0, 2, 1, 3)

@@ -1,0 +1,262 @@
+"""Local causal-LM prompt generator (models/lm.py) and the remote-generation parity path
+(runtime/remote.py).  CPU tests run the fp32 reference ops; the GPU tests at the bottom check
+the HIP decode kernels (GEMV, RMSNorm, RoPE+KV append, split-KV GQA decode attention) against the
+same references and the hipGraph-captured decode loop against eager decoding."""
+import asyncio
+import io
+import json
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from cassmantle_amd.models.lm import TINY_LM, CausalLM, CausalLMConfig, LMTextGenerator
+
+
+def _incremental_vs_full(m, tokens, prefix):
+    full = m.full_logits(tokens)
+    kc, vc = m.alloc_cache(tokens.shape[0], 64)
+    dev = tokens.device
+    pos = torch.zeros(tokens.shape[0], dtype=torch.int32, device=dev)
+    errs = [(m(tokens[:, :prefix], kc, vc, pos, decode=False).float() - full[:, prefix - 1]).abs().max().item()]
+    for t in range(prefix, tokens.shape[1]):
+        pos = torch.full((tokens.shape[0],), t, dtype=torch.int32, device=dev)
+        lg = m(tokens[:, t:t + 1], kc, vc, pos, pos + 1, decode=True).float()
+        errs.append((lg - full[:, t]).abs().max().item())
+    return errs, full.abs().max().item()
+
+
+def test_lm_incremental_decode_matches_full_forward():
+    m = CausalLM(TINY_LM, seed=1)
+    tokens = torch.randint(0, TINY_LM.vocab, (1, 12), generator=torch.Generator().manual_seed(0))
+    errs, scale = _incremental_vs_full(m, tokens, 8)
+    assert max(errs) < 0.03 * scale, (errs, scale)
+
+
+def test_lm_generator_token_budget():
+    g = LMTextGenerator(TINY_LM, device="cpu", seed=3)
+    ids = g.generate_ids([256, 72, 105], 6, 6)
+    assert len(ids) == 6                       # EOS suppressed until min_new_tokens
+    ids2 = g.generate_ids([256, 72, 105], 0, 5)
+    assert len(ids2) <= 5
+    assert isinstance(g.generate_text("The lantern", 2, 8), str)
+
+
+def test_lm_prompt_generator_keeps_two_sentence_contract():
+    from cassmantle_amd.game.prompts import LMPromptGenerator
+    pg = LMPromptGenerator(LMTextGenerator(TINY_LM, device="cpu"), min_new_tokens=4, max_new_tokens=12)
+    out = pg.generate("The Clockwork Orchard", True)
+    assert out.endswith(".") and out.count(".") >= 1
+
+
+def test_lm_checkpoint_roundtrip():
+    from cassmantle_amd.models.weights import export_causal_lm, load_causal_lm
+    a, b = CausalLM(TINY_LM, seed=1), CausalLM(TINY_LM, seed=2)
+    sd = export_causal_lm(a)
+    assert "model.layers.0.self_attn.k_proj.weight" in sd and "model.layers.1.mlp.gate_proj.weight" in sd
+    assert load_causal_lm(b, sd) == []
+    for (na, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(pa, pb), na
+
+
+def test_factory_builds_lm_prompt_generator():
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.game.prompts import LMPromptGenerator
+    from cassmantle_amd.runtime.factory import build_prompt_generator
+    cfg = Config()
+    assert build_prompt_generator(cfg) is None
+    cfg.set("prompt_generator", "lm")
+    cfg.set("device", "cpu")
+    assert isinstance(build_prompt_generator(cfg, device="cpu"), LMPromptGenerator)
+
+
+# ----------------------------------------------------------------------------- remote (api_call parity)
+class _FakeEndpoint:
+    """aiohttp test server: answers 503 ``fail_first`` times, then ``body``."""
+
+    def __init__(self, body: bytes, fail_first: int = 0, status: int = 503):
+        from aiohttp import web
+        self.body, self.fail_first, self.status, self.calls, self.payloads = body, fail_first, status, 0, []
+        app = web.Application()
+        app.router.add_post("/", self.handle)
+        self.runner = web.AppRunner(app)
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        self.port = s.getsockname()[1]
+        s.close()
+        self.loop = asyncio.new_event_loop()
+        self.thread = threading.Thread(target=self._serve, daemon=True)
+        self.ready = threading.Event()
+        self.thread.start()
+        self.ready.wait(10)
+
+    def _serve(self):
+        from aiohttp import web
+        asyncio.set_event_loop(self.loop)
+        self.loop.run_until_complete(self.runner.setup())
+        self.loop.run_until_complete(web.TCPSite(self.runner, "127.0.0.1", self.port).start())
+        self.ready.set()
+        self.loop.run_forever()
+
+    async def handle(self, request):
+        from aiohttp import web
+        self.calls += 1
+        self.payloads.append(await request.json())
+        if self.calls <= self.fail_first:
+            return web.Response(status=self.status, text="loading")
+        return web.Response(body=self.body)
+
+    @property
+    def url(self):
+        return f"http://127.0.0.1:{self.port}/"
+
+    def close(self):
+        fut = asyncio.run_coroutine_threadsafe(self.runner.cleanup(), self.loop)
+        fut.result(10)
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(10)
+
+
+def test_remote_prompt_retries_503_then_postprocesses():
+    from cassmantle_amd.runtime.remote import RemotePromptGenerator
+    seed = "The Clockwork Orchard"
+    body = json.dumps([{"generated_text": seed + " The gears sang. Apples of brass fell. Night came."}]).encode()
+    ep = _FakeEndpoint(body, fail_first=2)
+    try:
+        g = RemotePromptGenerator(ep.url, retry_unit_s=0.01, max_retries=5, token="tok")
+        assert g.generate(seed, True) == " The gears sang. Apples of brass fell."
+        assert ep.calls == 3
+        assert ep.payloads[0] == {"inputs": seed, "parameters": {"min_new_tokens": 32, "max_new_tokens": 96}}
+    finally:
+        ep.close()
+
+
+def test_remote_gives_up_after_max_retries_and_on_other_errors():
+    from cassmantle_amd.runtime.remote import RemotePromptGenerator
+    ep = _FakeEndpoint(b"[]", fail_first=100)
+    try:
+        assert RemotePromptGenerator(ep.url, retry_unit_s=0.0, max_retries=3).generate("x", True) is None
+        assert ep.calls == 3
+    finally:
+        ep.close()
+    ep = _FakeEndpoint(b"[]", fail_first=100, status=500)    # non-retryable status: abort at once
+    try:
+        assert RemotePromptGenerator(ep.url, retry_unit_s=0.0, max_retries=3).generate("x", True) is None
+        assert ep.calls == 1
+    finally:
+        ep.close()
+
+
+def test_remote_image_generator_decodes_bytes():
+    from PIL import Image
+    from cassmantle_amd.runtime.remote import RemoteImageGenerator
+    buf = io.BytesIO()
+    Image.new("RGB", (32, 24), (10, 200, 30)).save(buf, format="JPEG")
+    ep = _FakeEndpoint(buf.getvalue(), fail_first=1)
+    try:
+        imgs = RemoteImageGenerator(ep.url, retry_unit_s=0.0).generate(["a cat"], "blurry", [1])
+        assert imgs[0].shape == (24, 32, 3) and imgs[0].dtype == np.uint8
+        assert ep.payloads[-1] == {"inputs": "a cat", "parameters": {"negative_prompt": "blurry"}}
+    finally:
+        ep.close()
+
+
+# ----------------------------------------------------------------------------- GPU
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.fixture
+def hip():
+    from cassmantle_amd import ops
+    from cassmantle_amd.ops._ext import ext_available, ext_error
+    assert ext_available(), ext_error()
+    ops.set_mode("hip")
+    return ops
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("act", [None, "silu", "swiglu", "geglu"])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 1280), (320, 256)])
+def test_gemv_skinny_m(hip, M, act, N, K):
+    from cassmantle_amd.ops import reference as ref
+    g = torch.Generator().manual_seed(M * 7 + N)
+    Nw = 2 * N if act in ("swiglu", "geglu") else N
+    x = torch.randn(M, K, generator=g).bfloat16().cuda()
+    w = (torch.randn(Nw, K, generator=g) * K ** -0.5).bfloat16().cuda()
+    b = (torch.randn(Nw, generator=g) * 0.1).bfloat16().cuda()
+    r = torch.randn(M, N, generator=g).bfloat16().cuda()
+    y = hip.linear(x, w, b, residual=r, act=act)
+    assert _rel(y, ref.linear(x, w, b, residual=r, act=act)) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [256, 1024, 4096])
+def test_rms_norm(hip, D):
+    from cassmantle_amd.ops import reference as ref
+    x = torch.randn(37, D).bfloat16().cuda() * 3
+    w = torch.rand(D).bfloat16().cuda() + 0.5
+    assert _rel(hip.rms_norm(x, w, 1e-5), ref.rms_norm(x, w, 1e-5)) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,H,Hk,d", [(1, 7, 32, 8, 128), (2, 1, 4, 2, 64), (3, 5, 8, 8, 64)])
+def test_rope_kv(hip, B, T, H, Hk, d):
+    from cassmantle_amd.ops import reference as ref
+    L = 64
+    qkv = torch.randn(B, T, (H + 2 * Hk) * d).bfloat16().cuda()
+    pos0 = torch.tensor([3 * b + (0 if T > 1 else 40) for b in range(B)], dtype=torch.int32).cuda()
+    outs = []
+    for mode in ("hip", "ref"):
+        q = torch.zeros(B, T, H, d, dtype=torch.bfloat16, device="cuda")
+        kc = torch.zeros(B, L, Hk, d, dtype=torch.bfloat16, device="cuda")
+        vc = torch.zeros_like(kc)
+        if mode == "hip":
+            hip.rope_kv(qkv, pos0, q, kc, vc, H, Hk, 10000.0)
+        else:
+            ref.rope_kv(qkv, pos0, q, kc, vc, H, Hk, 10000.0)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Hk,d,L", [(1, 32, 8, 128, 512), (2, 4, 2, 64, 256), (3, 8, 8, 64, 100), (1, 8, 1, 128, 4096)])
+def test_decode_attention(hip, B, H, Hk, d, L):
+    from cassmantle_amd.ops import reference as ref
+    q = torch.randn(B, H, d).bfloat16().cuda()
+    kc = torch.randn(B, L, Hk, d).bfloat16().cuda()
+    vc = torch.randn(B, L, Hk, d).bfloat16().cuda()
+    lens = torch.tensor([max(1, L - 37 * b - 5) for b in range(B)], dtype=torch.int32).cuda()
+    o = hip.decode_attention(q, kc, vc, lens)
+    assert _rel(o, ref.decode_attention(q, kc, vc, lens, d ** -0.5)) < 2e-2
+
+
+@pytest.mark.gpu
+def test_attention_gqa_causal(hip):
+    from cassmantle_amd.ops import reference as ref
+    q = torch.randn(2, 50, 8, 64).bfloat16().cuda()
+    k = torch.randn(2, 50, 2, 64).bfloat16().cuda()
+    v = torch.randn(2, 50, 2, 64).bfloat16().cuda()
+    assert _rel(hip.attention(q, k, v, causal=True), ref.attention(q, k, v, causal=True)) < 2e-2
+
+
+@pytest.mark.gpu
+def test_lm_gpu_decode_and_graph(hip):
+    cfg = CausalLMConfig("mid", 1000, 512, 3, 8, 2, 1024, 10000.0, 1e-5, 256)
+    m = CausalLM(cfg, device="cuda", seed=4)
+    tokens = torch.randint(0, cfg.vocab, (1, 20), generator=torch.Generator().manual_seed(1)).cuda()
+    errs, scale = _incremental_vs_full(m, tokens, 12)
+    assert max(errs) < 0.05 * scale, (errs, scale)
+    eager = LMTextGenerator(cfg, device="cuda", seed=5, use_graphs=False)
+    graph = LMTextGenerator(cfg, device="cuda", seed=5, use_graphs=True)
+    a = eager.generate_ids([256, 10, 20, 30], 24, 24)
+    b = graph.generate_ids([256, 10, 20, 30], 24, 24)
+    assert graph.graph is not None
+    assert len(a) == len(b) == 24
+    assert sum(x == y for x, y in zip(a, b)) >= 20   # bf16 near-ties may flip a late sample
+    c = graph.generate_ids([256, 10, 20, 30], 24, 24)   # graph replays with fresh noise / state
+    assert len(c) == 24
