@@ -106,8 +106,7 @@ class LMBlock(nn.Module):
         c = self.c
         B, T, _ = x.shape
         hd = c.head_dim
-        n = ops.rms_norm(x, self.attn_norm, c.eps)
-        qkv = ops.linear(n, self.qkv)
+        qkv = ops.rms_linear(x, self.attn_norm, c.eps, self.qkv)
         q = torch.empty((B, T, c.heads, hd), device=x.device, dtype=x.dtype)
         ops.rope_kv(qkv, pos0, q, kc, vc, c.heads, c.kv_heads, c.rope_theta)
         if decode:
@@ -116,8 +115,7 @@ class LMBlock(nn.Module):
             # prefill from position 0: causal flash attention over the freshly written cache rows
             o = ops.attention(q, kc[:, :T], vc[:, :T], causal=True)
         x = ops.linear(o.reshape(B, T, c.heads * hd), self.o, residual=x)
-        n = ops.rms_norm(x, self.mlp_norm, c.eps)
-        h = ops.linear(n, self.gate_up, act="swiglu")
+        h = ops.rms_linear(x, self.mlp_norm, c.eps, self.gate_up, act="swiglu")
         return ops.linear(h, self.down, residual=x)
 
 
@@ -146,8 +144,7 @@ class CausalLM(nn.Module):
         x = self.embed.index_select(0, tokens.reshape(-1)).view(B, T, self.c.dim)
         for i, blk in enumerate(self.blocks):
             x = blk(x, kcache[i], vcache[i], pos0, lens, decode)
-        x = ops.rms_norm(x[:, -1], self.norm, self.c.eps)
-        return ops.linear(x, self.lm_head)
+        return ops.rms_linear(x[:, -1], self.norm, self.c.eps, self.lm_head)
 
     @torch.no_grad()
     def full_logits(self, tokens: torch.Tensor) -> torch.Tensor:

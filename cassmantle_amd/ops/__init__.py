@@ -168,6 +168,25 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     return out
 
 
+def rms_linear(x: torch.Tensor, gamma: torch.Tensor, eps: float, w: torch.Tensor,
+               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+               act: Optional[str] = None) -> torch.Tensor:
+    """linear(rms_norm(x, gamma), w, ...).  For <= 8 rows (decode) the norm runs inside the
+    weight-streaming GEMV (row statistics from the same loads); otherwise two kernels."""
+    K = x.shape[-1]
+    rows = x.numel() // K
+    if not _use_hip(x) or rows > 8 or K % 8:
+        return linear(rms_norm(x, gamma, eps), w, bias, residual=residual, act=act)
+    x2 = x.reshape(rows, K)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    N = w.shape[0] // 2 if act in ("geglu", "swiglu") else w.shape[0]
+    out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
+    r2 = residual.reshape(rows, N) if residual is not None else None
+    ext().gemm_rms(x2, gamma, float(eps), w, bias, r2, out, _ACT[act])
+    return out.reshape(*x.shape[:-1], N)
+
+
 # ----------------------------------------------------------------------------- causal-LM decode path
 def rope_kv(qkv: torch.Tensor, pos0: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
             v_cache: torch.Tensor, heads: int, kv_heads: int, theta: float) -> None:

@@ -65,6 +65,27 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   run_gemm(p, out);
 }
 
+// y = act(rmsnorm(x) @ w^T + bias) + residual for skinny x (<= 8 rows): the norm is fused into
+// the weight-streaming GEMV (decode path of the causal LM)
+void gemm_rms(const at::Tensor& x, const at::Tensor& gamma, double eps, const at::Tensor& w,
+              const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, at::Tensor& out,
+              int64_t act) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(gamma); CHECK_CONTIG(gamma); CHECK_BF16(w); CHECK_CONTIG(w);
+  CHECK_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(0) <= 8, "gemm_rms: x [<=8, K] rows contiguous");
+  GemmArgs p;
+  p.A = bptr(x); p.W = bptr(w); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
+  p.M = (int)x.size(0); p.K = (int)x.size(1); p.N = (int)out.size(1); p.Nw = (int)w.size(0);
+  p.lda = (int)x.stride(0); p.ldc = p.N; p.act = (int)act;
+  p.rms_gamma = bptr(gamma); p.rms_eps = (float)eps;
+  TORCH_CHECK(gamma.numel() == p.K && w.size(1) == p.K, "gemm_rms: K mismatch");
+  TORCH_CHECK(p.Nw == ((act == 4 || act == 6) ? 2 * p.N : p.N), "gemm_rms: N mismatch");
+  if (out.scalar_type() == at::kFloat) p.out_f32 = 1;
+  else CHECK_BF16(out);
+  p.C = out.data_ptr();
+  TORCH_CHECK(launch_gemv(p, cur_stream()), "gemm_rms: shape not supported by the GEMV path (K % 8)");
+}
+
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
             const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& chan_bias, at::Tensor& out,
             int64_t stride, int64_t pad, int64_t upsample) {
@@ -298,9 +319,18 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
   const int ns = decode_splits(a.B, a.Hk, a.L);
   at::Tensor ws;
   a.ws = nullptr;
+  a.tickets = nullptr;
   if (ns > 1) {
     ws = at::empty({(long long)a.B * a.H * ns * (a.d + 2)}, q.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
+    // arrival tickets: zeroed once per device, every kernel re-arms the ones it used
+    static std::vector<at::Tensor> tickets;
+    const int dev = q.get_device();
+    if ((int)tickets.size() <= dev) tickets.resize(dev + 1);
+    // never reallocated: a captured graph keeps pointing at it
+    if (!tickets[dev].defined()) tickets[dev] = at::zeros({65536}, q.options().dtype(at::kInt));
+    TORCH_CHECK((long long)a.B * a.Hk <= 65536, "decode_attention: B * kv_heads <= 65536");
+    a.tickets = tickets[dev].data_ptr<int>();
   }
   launch_decode_attention(a, ns, cur_stream());
 }
@@ -310,6 +340,7 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
   m.def("gemm", &gemm);
+  m.def("gemm_rms", &gemm_rms);
   m.def("conv2d", &conv2d);
   m.def("bmm_nt", &bmm_nt);
   m.def("group_norm", &group_norm);

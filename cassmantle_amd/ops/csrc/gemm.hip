@@ -561,8 +561,8 @@ GemmPlan gemm_plan(const GemmArgs& p) {
   GemmPlan best{0, 1};
   if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) return best;
   const int nk = (p.K + BK - 1) / BK;
-  // tiny-M GEMMs (time-embedding / pooled projections) are launch-bound: never split them
-  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M >= 128;
+  // M <= 8 goes to the GEMV path; short prompts (M = tens of rows) need split-K to fill the chip
+  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M > 8;
   double best_t = 1e30;
   for (int c = 0; c < 5; ++c) {
     const TileCfg& tc = kTiles[c];

@@ -23,6 +23,9 @@ struct GemmArgs {
   int cfg = 0;                         // tile config index (gemm_plan)
   // implicit-GEMM convolution (conv != 0)
   int conv = 0, IH = 0, IW = 0, Cin = 0, Ho = 0, Wo = 0, stride = 1, pad = 0, ksize = 1, upsample = 0;
+  // fused RMSNorm of A's rows (GEMV path only): A <- A * gamma / rms(A)
+  const uint16_t* rms_gamma = nullptr;
+  float rms_eps = 0.f;
 };
 #define GEMM_MAX_SPLIT 16
 struct GemmPlan { int cfg; int split; };
@@ -71,6 +74,7 @@ struct DecodeArgs {
   const int* lens;                     // [B] valid keys (device)
   uint16_t* o; long long o_sb;         // [B][H][d]
   float* ws;                           // split partials [B*H][ns][d+2]
+  int* tickets;                        // [B*Hk] zeroed arrival counters (re-armed by the kernel)
   int B, H, Hk, d, L;
   float scale;
 };

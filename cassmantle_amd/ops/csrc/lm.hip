@@ -54,6 +54,35 @@ CM_DEVICE float transpose_reduce(float (&v)[V], int lane, int& idx) {
 template <int MM, bool GATED> constexpr int gemv_r() { return (GATED && MM >= 8) ? 2 : 4; }
 constexpr int GEMV_THREADS = 256;
 
+// one 8-element k-chunk of every row: acc[r*MM+m] += A[m][k..k+7] . W[r][k..k+7]; with
+// gamma (fused RMSNorm) also ss[m] += A^2 and A is scaled by gamma first
+template <int MM, int NR>
+CM_DEVICE void gemv_chunk(const uint4 (&wv)[NR], const uint16_t* A, int lda, int M, int k, const uint16_t* gamma,
+                          float (&acc)[NR * MM], float (&ss)[MM]) {
+  float gf[8];
+  if (gamma) unpack8(*reinterpret_cast<const uint4*>(gamma + k), gf);
+#pragma unroll
+  for (int m = 0; m < MM; ++m) {
+    if (m < M) {
+      float af[8];
+      unpack8(*reinterpret_cast<const uint4*>(A + (long long)m * lda + k), af);
+      if (gamma) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ss[m] = fmaf(af[e], af[e], ss[m]); af[e] *= gf[e]; }
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        float wf[8];
+        unpack8(wv[r], wf);
+        float s = acc[r * MM + m];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s = fmaf(af[e], wf[e], s);
+        acc[r * MM + m] = s;
+      }
+    }
+  }
+}
+
 template <int MM, bool GATED>
 __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(GemmArgs p) {
   constexpr int GEMV_R = gemv_r<MM, GATED>();
@@ -76,49 +105,68 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(GemmArgs p) {
   float acc[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  // fused RMSNorm prologue (p.rms_gamma): the block covers all of K for its rows, so it owns the
+  // row statistics: sum(x^2) accumulates from the same A loads, gamma scales A in registers and
+  // 1/rms is applied to the finished dot products (no normalised copy of x in HBM)
+  const bool rms = p.rms_gamma != nullptr;
+  float ss[MM];
+#pragma unroll
+  for (int m = 0; m < MM; ++m) ss[m] = 0.f;
 
-  for (int k = (wave * 64 + lane) * 8; k < p.K; k += GEMV_THREADS * 8) {
-    uint4 wv[NR];
+  // two k-chunks per iteration: all 2*NR weight loads are issued before any FMA (the kernel is a
+  // pure HBM stream, no LDS staging)
+  constexpr int STEP = GEMV_THREADS * 8;
+  int k = (wave * 64 + lane) * 8;
+  for (; NR * MM <= 8 && k + STEP < p.K; k += 2 * STEP) {   // (wide blocks: keep occupancy)
+    uint4 w0[NR], w1[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) wv[r] = *reinterpret_cast<const uint4*>(wr[r] + k);
-    float wf[NR][8];
+    for (int r = 0; r < NR; ++r) w0[r] = *reinterpret_cast<const uint4*>(wr[r] + k);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) unpack8(wv[r], wf[r]);
+    for (int r = 0; r < NR; ++r) w1[r] = *reinterpret_cast<const uint4*>(wr[r] + k + STEP);
+    gemv_chunk<MM, NR>(w0, A, p.lda, p.M, k, p.rms_gamma, acc, ss);
+    gemv_chunk<MM, NR>(w1, A, p.lda, p.M, k + STEP, p.rms_gamma, acc, ss);
+  }
+  for (; k < p.K; k += STEP) {
+    uint4 w0[NR];
 #pragma unroll
-    for (int m = 0; m < MM; ++m) {
-      if (m < p.M) {
-        float af[8];
-        unpack8(*reinterpret_cast<const uint4*>(A + (long long)m * p.lda + k), af);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          float s = acc[r * MM + m];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s = fmaf(af[e], wf[r][e], s);
-          acc[r * MM + m] = s;
-        }
-      }
-    }
+    for (int r = 0; r < NR; ++r) w0[r] = *reinterpret_cast<const uint4*>(wr[r] + k);
+    gemv_chunk<MM, NR>(w0, A, p.lda, p.M, k, p.rms_gamma, acc, ss);
   }
 
   int idx;
   const float tot = transpose_reduce<V>(acc, lane, idx);
   __shared__ float red[GEMV_THREADS / 64][V];
+  __shared__ float red_ss[GEMV_THREADS / 64][MM];
   if ((lane & (64 / V - 1)) == 0) red[wave][idx] = tot;
+  if (rms) {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      const float v = wave_sum(ss[m]);
+      if (lane == 0) red_ss[wave][m] = v;
+    }
+  }
   __syncthreads();
   const int t = threadIdx.x;
   if (t >= GEMV_R * MM) return;
   const int r = t / MM, m = t - r * MM;
   const int n = n0 + r;
   if (n >= p.N || m >= p.M) return;
+  float scale = p.alpha;
+  if (rms) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < GEMV_THREADS / 64; ++w) s2 += red_ss[w][m];
+    scale *= rsqrtf(s2 / p.K + p.rms_eps);
+  }
   float o = 0.f;
 #pragma unroll
   for (int w = 0; w < GEMV_THREADS / 64; ++w) o += red[w][t];
-  o *= p.alpha;
+  o *= scale;
   if constexpr (GATED) {
     float g = 0.f;
 #pragma unroll
     for (int w = 0; w < GEMV_THREADS / 64; ++w) g += red[w][GEMV_R * MM + t];
-    g *= p.alpha;
+    g *= scale;
     if (p.bias) { o += bf2f(p.bias[n]); g += bf2f(p.bias[p.N + n]); }
     o = gate_f(o, g, p.act);
   } else {
@@ -181,60 +229,172 @@ __global__ void rope_kv_kernel(RopeArgs a) {
 }
 
 // --------------------------------------------------------------------------- decode attention
-constexpr int DEC_THREADS = 256;
+constexpr int DEC_THREADS = 128;   // 2 waves: a 64-key V tile per wave staged in LDS
 constexpr int DEC_MAXG = 8;
 
+// Merge per-split partials (m, l, acc[D]) of G heads -> normalised bf16 output
 template <int D>
+__device__ void decode_combine(const DecodeArgs& a, int b, int hk, int G, int ns, int nact) {
+  for (int i = threadIdx.x; i < G * D; i += DEC_THREADS) {
+    const int g = i / D, e = i - g * D;
+    const int h = hk * G + g;
+    const float* w = a.ws + (long long)(b * a.H + h) * ns * (D + 2);
+    float M = -INFINITY;
+#pragma unroll 4
+    for (int s = 0; s < nact; ++s) M = fmaxf(M, __builtin_nontemporal_load(w + s * (D + 2) + D));
+    float l = 0.f, o = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll 4
+      for (int s = 0; s < nact; ++s) {
+        const float c = exp2f(__builtin_nontemporal_load(w + s * (D + 2) + D) - M);
+        l += __builtin_nontemporal_load(w + s * (D + 2) + D + 1) * c;
+        o += __builtin_nontemporal_load(w + s * (D + 2) + e) * c;
+      }
+    }
+    a.o[(long long)b * a.o_sb + (long long)h * a.d + e] = f2bf(l > 0.f ? o / l : 0.f);
+  }
+}
+
+// grid (B*Hk, ns): block = one KV head of one sequence x one key span (multiple of 128 keys).
+// Scores with lane = key (each lane dots its K row with the G queries broadcast from LDS: all of
+// a row's 16-byte loads issue at once), one wave max/sum per 64 keys and head, then P.V with
+// lane = head-dim element over coalesced V rows.  Split partials are merged by the LAST block of
+// each (sequence, kv head) to finish (atomic ticket), so there is no second launch.
+template <int D, int G>
 __global__ __launch_bounds__(DEC_THREADS) void decode_attn_kernel(DecodeArgs a) {
-  constexpr int DL = D / 64;        // head-dim elements per lane
+  constexpr int DL = D / 64;          // head-dim elements per lane in P.V
+  constexpr int NW = DEC_THREADS / 64;
+  constexpr int NCH = D / 8;          // 16-byte chunks per K/V row
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x / a.Hk, hk = blockIdx.x - b * a.Hk;
-  const int G = a.H / a.Hk;
-  const int len = a.lens[b];
-  const int chunk = (a.L + gridDim.y - 1) / gridDim.y;
-  const int k0 = blockIdx.y * chunk;
-  const int k1 = min(len, k0 + chunk);
+  const int ns = gridDim.y;
+  const int span = ((a.L + ns - 1) / ns + NW * 64 - 1) / (NW * 64) * (NW * 64);
+  const int k0 = blockIdx.y * span;
+  const long long row = (long long)a.Hk * a.d;            // elements between consecutive keys
+  const uint16_t* Kb = a.k_cache + ((long long)b * a.L * a.Hk + hk) * a.d;
+  const uint16_t* Vb = a.v_cache + ((long long)b * a.L * a.Hk + hk) * a.d;
 
-  float q[DEC_MAXG][DL];
-  float m_run[DEC_MAXG], l_run[DEC_MAXG], acc[DEC_MAXG][DL];
-  const float qs = a.scale * 1.4426950408889634f;   // exp2 domain
+  // Decode is a latency chain: the length and the G query rows are fetched in one round.
+  const int len_raw = a.lens[b];
+  // the G query rows of this kv head are contiguous: [G*D] bf16, 4 per thread and round
+  const int nq4 = G * D / 4;
+  const uint16_t* qb = a.q + (long long)b * a.q_sb + (long long)hk * G * a.d;
+  const int i0 = threadIdx.x, i1 = threadIdx.x + DEC_THREADS;
+  const uint2 qv0 = i0 < nq4 ? *reinterpret_cast<const uint2*>(qb + 4 * i0) : make_uint2(0, 0);
+  const uint2 qv1 = i1 < nq4 ? *reinterpret_cast<const uint2*>(qb + 4 * i1) : make_uint2(0, 0);
+  const int len = min(len_raw, a.L);
+  const int k1 = min(len, k0 + span);
+  // only the splits that hold keys take part (short contexts: one block, no merge at all)
+  const int nact = min(ns, (len + span - 1) / span);
+  if (blockIdx.y >= max(nact, 1)) return;
+  if (nact == 0) {
+    for (int i = threadIdx.x; i < G * D; i += DEC_THREADS)
+      a.o[(long long)b * a.o_sb + (long long)(hk * G + i / D) * a.d + i % D] = 0;
+    return;
+  }
+
+  __shared__ float qs[G][D];
+  __shared__ float ps[NW][G][64];
+  __shared__ uint4 vs[NW][64][NCH + 1];   // +16 B row pad: conflict-light stores, free row reads
+  const float qscale = a.scale * 1.4426950408889634f;   // exp2 domain
+  float* qsf = &qs[0][0];
+  if (i0 < nq4) {
+    qsf[4 * i0 + 0] = __uint_as_float(qv0.x << 16) * qscale;
+    qsf[4 * i0 + 1] = __uint_as_float(qv0.x & 0xffff0000u) * qscale;
+    qsf[4 * i0 + 2] = __uint_as_float(qv0.y << 16) * qscale;
+    qsf[4 * i0 + 3] = __uint_as_float(qv0.y & 0xffff0000u) * qscale;
+  }
+  if (i1 < nq4) {
+    qsf[4 * i1 + 0] = __uint_as_float(qv1.x << 16) * qscale;
+    qsf[4 * i1 + 1] = __uint_as_float(qv1.x & 0xffff0000u) * qscale;
+    qsf[4 * i1 + 2] = __uint_as_float(qv1.y << 16) * qscale;
+    qsf[4 * i1 + 3] = __uint_as_float(qv1.y & 0xffff0000u) * qscale;
+  }
+  __syncthreads();
+
+  float m_run[G], l_run[G], acc[G][DL];
 #pragma unroll
-  for (int g = 0; g < DEC_MAXG; ++g) {
+  for (int g = 0; g < G; ++g) {
     m_run[g] = -INFINITY; l_run[g] = 0.f;
 #pragma unroll
-    for (int e = 0; e < DL; ++e) {
-      acc[g][e] = 0.f;
-      q[g][e] = g < G ? bf2f(a.q[(long long)b * a.q_sb + (long long)(hk * G + g) * a.d + lane * DL + e]) * qs : 0.f;
-    }
+    for (int e = 0; e < DL; ++e) acc[g][e] = 0.f;
   }
-  for (int key = k0 + wave; key < k1; key += DEC_THREADS / 64) {
-    const long long base = (((long long)b * a.L + key) * a.Hk + hk) * a.d + lane * DL;
-    float kf[DL], vf[DL];
+
+  for (int t0 = k0 + wave * 64; t0 < k1; t0 += NW * 64) {
+    const bool valid = t0 + lane < k1;
+    // this lane's whole K and V rows in flight at once (one memory latency per 64-key tile)
+    uint4 kv[NCH], vv[NCH];
+    {
+      const long long ro = (long long)min(t0 + lane, a.L - 1) * row;
 #pragma unroll
-    for (int e = 0; e < DL; ++e) { kf[e] = bf2f(a.k_cache[base + e]); vf[e] = bf2f(a.v_cache[base + e]); }
+      for (int c = 0; c < NCH; ++c) kv[c] = reinterpret_cast<const uint4*>(Kb + ro)[c];
 #pragma unroll
-    for (int g = 0; g < DEC_MAXG; ++g) {
-      if (g < G) {
-        float s = 0.f;
+      for (int c = 0; c < NCH; ++c) vv[c] = reinterpret_cast<const uint4*>(Vb + ro)[c];
+    }
+    float sc[G];
 #pragma unroll
-        for (int e = 0; e < DL; ++e) s = fmaf(q[g][e], kf[e], s);
-        s = wave_sum(s);
-        const float mn = fmaxf(m_run[g], s);
+    for (int g = 0; g < G; ++g) sc[g] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      float kf[8];
+      unpack8(kv[c], kf);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sc[g] = fmaf(qs[g][c * 8 + e], kf[e], sc[g]);
+        }
+      }
+    }
+    // V tile -> LDS (row = key) for the P.V pass over head-dim lanes
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) vs[wave][lane][c] = vv[c];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      {
+        const float s = valid ? sc[g] : -INFINITY;
+        const float mn = fmaxf(m_run[g], wave_max(s));    // lane 0 is always a valid key
         const float corr = exp2f(m_run[g] - mn);
-        const float pr = exp2f(s - mn);
-        l_run[g] = l_run[g] * corr + pr;
+        const float p = exp2f(s - mn);
+        l_run[g] = l_run[g] * corr + wave_sum(p);
+        ps[wave][g][lane] = p;
 #pragma unroll
-        for (int e = 0; e < DL; ++e) acc[g][e] = fmaf(acc[g][e], corr, pr * vf[e]);
+        for (int e = 0; e < DL; ++e) acc[g][e] *= corr;
         m_run[g] = mn;
       }
     }
-  }
-  // merge the 4 waves
-  __shared__ float sm[DEC_THREADS / 64][DEC_MAXG], sl[DEC_THREADS / 64][DEC_MAXG];
-  __shared__ float sacc[DEC_THREADS / 64][DEC_MAXG][D];
+    __builtin_amdgcn_wave_barrier();
+    const int nv = min(64, k1 - t0);
+    const int mych = (lane * DL) / 8, myoff = (lane * DL) & 7;   // this lane's d elements
+#pragma unroll 8
+    for (int j = 0; j < nv; ++j) {
+      const uint16_t* rp = reinterpret_cast<const uint16_t*>(&vs[wave][j][mych]) + myoff;
+      float vf[DL];
+      if constexpr (DL == 2) {
+        const uint32_t u = *reinterpret_cast<const uint32_t*>(rp);
+        vf[0] = __uint_as_float(u << 16);
+        vf[1] = __uint_as_float(u & 0xffff0000u);
+      } else {
+        vf[0] = bf2f(*rp);
+      }
 #pragma unroll
-  for (int g = 0; g < DEC_MAXG; ++g) {
-    if (g < G) {
+      for (int g = 0; g < G; ++g) {
+        {
+          const float pj = ps[wave][g][j];
+#pragma unroll
+          for (int e = 0; e < DL; ++e) acc[g][e] = fmaf(pj, vf[e], acc[g][e]);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // merge the waves of this block
+  __shared__ float sm[NW][G], sl[NW][G];
+  __shared__ float sacc[NW][G][D];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    {
       if (lane == 0) { sm[wave][g] = m_run[g]; sl[wave][g] = l_run[g]; }
 #pragma unroll
       for (int e = 0; e < DL; ++e) sacc[wave][g][lane * DL + e] = acc[g][e];
@@ -245,45 +405,39 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_attn_kernel(DecodeArgs a) 
     const int g = i / D, e = i - g * D;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < DEC_THREADS / 64; ++w) M = fmaxf(M, sm[w][g]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sm[w][g]);
     float l = 0.f, o = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < DEC_THREADS / 64; ++w) {
+      for (int w = 0; w < NW; ++w) {
         const float c = exp2f(sm[w][g] - M);
         l += sl[w][g] * c;
         o += sacc[w][g][e] * c;
       }
     }
     const int h = hk * G + g;
-    if (gridDim.y == 1) {
+    if (nact == 1) {
       a.o[(long long)b * a.o_sb + (long long)h * a.d + e] = f2bf(l > 0.f ? o / l : 0.f);
     } else {
-      const long long slot = ((long long)(b * a.H + h) * gridDim.y + blockIdx.y);
-      a.ws[slot * (D + 2) + e] = o;
-      if (e == 0) { a.ws[slot * (D + 2) + D] = M; a.ws[slot * (D + 2) + D + 1] = l; }
+      float* w = a.ws + ((long long)(b * a.H + h) * ns + blockIdx.y) * (D + 2);
+      w[e] = o;
+      if (e == 0) { w[D] = M; w[D + 1] = l; }
     }
   }
-}
-
-template <int D>
-__global__ void decode_combine_kernel(DecodeArgs a, int ns) {
-  const int bh = blockIdx.x;                 // b * H + h
-  const int b = bh / a.H, h = bh - b * a.H;
-  const int e = threadIdx.x;
-  if (e >= D) return;
-  const float* w = a.ws + (long long)bh * ns * (D + 2);
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, w[s * (D + 2) + D]);
-  float l = 0.f, o = 0.f;
-  if (M != -INFINITY) {
-    for (int s = 0; s < ns; ++s) {
-      const float c = exp2f(w[s * (D + 2) + D] - M);
-      l += w[s * (D + 2) + D + 1] * c;
-      o += w[s * (D + 2) + e] * c;
-    }
+  if (nact == 1) return;
+  // last block of this (b, hk) to finish merges the splits and re-arms the ticket
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = atomicAdd(a.tickets + blockIdx.x, 1);
+    last = (t == nact - 1);
+    if (last) a.tickets[blockIdx.x] = 0;
   }
-  a.o[(long long)b * a.o_sb + (long long)h * a.d + e] = f2bf(l > 0.f ? o / l : 0.f);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  decode_combine<D>(a, b, hk, G, ns, nact);
 }
 
 }  // namespace
@@ -306,21 +460,31 @@ void launch_rope_kv(const RopeArgs& a, hipStream_t s) {
 }
 
 int decode_splits(int B, int Hk, int L) {
-  // enough blocks to cover the CUs for batch-1 decode, >= 64 keys per split
-  int want = (512 + B * Hk - 1) / (B * Hk);
-  int maxs = (L + 63) / 64;
-  int ns = want < maxs ? want : maxs;
+  // one split per 128 keys (one 64-key tile per wave), at most 32
+  (void)B; (void)Hk;
+  int ns = (L + 127) / 128;
   if (ns > 32) ns = 32;
   return ns < 1 ? 1 : ns;
 }
 
+template <int D>
+static void launch_dec_d(const DecodeArgs& a, dim3 grid, hipStream_t s) {
+  // the query-group size is a template argument: the score loop is then a fixed unrolled set of
+  // broadcast LDS reads + FMAs (no per-head branches)
+  switch (a.H / a.Hk) {
+    case 1: hipLaunchKernelGGL((decode_attn_kernel<D, 1>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((decode_attn_kernel<D, 2>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((decode_attn_kernel<D, 3>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((decode_attn_kernel<D, 4>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((decode_attn_kernel<D, 5>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((decode_attn_kernel<D, 6>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((decode_attn_kernel<D, 7>), grid, dim3(DEC_THREADS), 0, s, a); break;
+    default: hipLaunchKernelGGL((decode_attn_kernel<D, 8>), grid, dim3(DEC_THREADS), 0, s, a); break;
+  }
+}
+
 void launch_decode_attention(const DecodeArgs& a, int ns, hipStream_t s) {
   dim3 grid(a.B * a.Hk, ns);
-  if (a.d == 64) {
-    hipLaunchKernelGGL(decode_attn_kernel<64>, grid, dim3(DEC_THREADS), 0, s, a);
-    if (ns > 1) hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(a.B * a.H), dim3(64), 0, s, a, ns);
-  } else {
-    hipLaunchKernelGGL(decode_attn_kernel<128>, grid, dim3(DEC_THREADS), 0, s, a);
-    if (ns > 1) hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(a.B * a.H), dim3(128), 0, s, a, ns);
-  }
+  if (a.d == 64) launch_dec_d<64>(a, grid, s);
+  else launch_dec_d<128>(a, grid, s);
 }

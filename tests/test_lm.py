@@ -194,6 +194,22 @@ def test_gemv_skinny_m(hip, M, act, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 4, 8])
+@pytest.mark.parametrize("act", [None, "swiglu"])
+def test_rms_linear_fused(hip, M, act):
+    from cassmantle_amd.ops import reference as ref
+    g = torch.Generator().manual_seed(M)
+    K, N = 4096, 1536
+    x = (torch.randn(M, K, generator=g) * 3).bfloat16().cuda()
+    gam = (torch.rand(K, generator=g) + 0.5).bfloat16().cuda()
+    w = (torch.randn(2 * N if act else N, K, generator=g) * K ** -0.5).bfloat16().cuda()
+    r = torch.randn(M, N, generator=g).bfloat16().cuda()
+    y = hip.rms_linear(x, gam, 1e-5, w, residual=r, act=act)
+    want = ref.linear(ref.rms_norm(x, gam, 1e-5), w, residual=r, act=act)
+    assert _rel(y, want) < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D", [256, 1024, 4096])
 def test_rms_norm(hip, D):
     from cassmantle_amd.ops import reference as ref
