@@ -24,6 +24,8 @@ import sys
 import time
 
 BASELINE_IMAGES_PER_SEC = None  # BASELINE.json "published": {} — no reference number
+METRICS = {"sd15": "SD-1.5 512^2 50-step images/sec (whole node) + p50 guess-score latency",
+           "sdxl": "SDXL-base 1024^2 30-step images/sec (BASELINE config 4)"}
 
 
 def parse():
@@ -33,8 +35,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--batch", type=int, default=4, help="images per room (per GPU)")
     p.add_argument("--model", default="sd15")
-    p.add_argument("--denoise-steps", type=int, default=50)
-    p.add_argument("--scheduler", default="pndm")
+    p.add_argument("--denoise-steps", type=int, default=None, help="default: the model spec's (sd15: 50)")
+    p.add_argument("--scheduler", default=None, help="default: the model spec's (sd15: pndm)")
     p.add_argument("--baseline", action="store_true", help="stock PyTorch ops, no graphs (eager baseline)")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--no-score", action="store_true")
@@ -64,6 +66,8 @@ def main() -> int:
     torch.manual_seed(0)
 
     spec = SPECS[args.model]
+    args.denoise_steps = args.denoise_steps or spec.steps
+    args.scheduler = args.scheduler or spec.scheduler
     sd = StableDiffusion(spec, device=device, use_graphs=not (args.baseline or args.no_graphs),
                          fp8_attention=args.fp8_attention, seed=0)
     gen = SyntheticPromptGenerator(salt=rank)
@@ -136,7 +140,7 @@ def main() -> int:
         images = world * args.batch * args.steps
         value = images / elapsed
         out = {
-            "metric": "SD-1.5 512^2 50-step images/sec (whole node) + p50 guess-score latency",
+            "metric": METRICS.get(args.model, f"{args.model} images/sec"),
             "value": round(value, 4),
             "unit": "images/s",
             "n_gpus": world,
@@ -148,8 +152,9 @@ def main() -> int:
             "vs_baseline": (value / BASELINE_IMAGES_PER_SEC) if BASELINE_IMAGES_PER_SEC else None,
             "dtype": "bf16",
             "data": "synthetic (seeds.txt template prompts, random-init weights)",
-            "config": {"model": f"{args.model} UNet/VAE/CLIP-L ({spec.resolution}x{spec.resolution}, "
-                                f"{args.denoise_steps} steps {args.scheduler}, cfg 7.5)",
+            "config": {"model": f"{args.model} UNet/VAE/CLIP ({spec.resolution}x{spec.resolution}, "
+                                f"{args.denoise_steps} steps {args.scheduler}, cfg {spec.guidance})"
+                                + (", fp8 attention" if args.fp8_attention else ""),
                        "global_batch": world * args.batch, "seq_len": (spec.resolution // 8) ** 2,
                        "parallelism": f"dp{world} (rooms)"},
             "ops": "torch-eager" if args.baseline else "hip",

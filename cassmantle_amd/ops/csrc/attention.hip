@@ -334,7 +334,268 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
   else launch_t<DQK, DO, 2>(a, s);
 }
 
+// ================================================================================ fp8 (OCP e4m3)
+// BASELINE config 4 (SDXL, head dim 64): both attention GEMMs on the block-scaled fp8 MFMA
+// v_mfma_scale_f32_32x32x64_f8f6f4 (scales fixed at 2^0), which does a 32x32 tile over 64 head
+// dims / 64 keys in ONE instruction at twice the bf16 rate:
+//   S^T = K8 . Q8^T       A = 32 key rows x 64 d (32 B per lane from LDS), B = Q8 in registers
+//   O^T += V8^T . P8^T    B = P^T from the S accumulator (fp8 packed, k order = accumulator order)
+//                         A = V^T rows from a pre-transposed fp8 V whose 64-key blocks are stored
+//                             in exactly that k order, so the A fragment is 32 contiguous bytes.
+// K and V are packed once per call by attn_fp8_pack_kernel (K8 [B,Hk,Nkp,64], V8t [B,Hk,64,Nkp],
+// Nkp = keys rounded up to 64, zero padded); Q is quantised in registers after the
+// scale*log2(e) prescale.  P <= 2^RESCALE_THR (deferred max) stays inside e4m3's range.
+// Element j (0..31) of lane half h of a 32x32x64 operand is paired with the same (h, j) of the
+// other operand, so only the P <-> V^T correspondence has to be fixed: slot 32h + j of a key
+// block holds key kappa(h, j) = 32(j>>4) + (j&3) + 8((j&15)>>2) + 4h, the key of S accumulator
+// register j&15 of key-half j>>4 in lane half h.
+constexpr int F8_KSTR = 80;   // LDS row stride (bytes) of the 64-byte fp8 rows: 16-lane groups
+                              // of ds_read_b128 hit disjoint banks (20 r mod 64 distinct)
+
+CM_DEVICE uint32_t f8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+// slot of key offset kk (0..63) inside its 64-key block of V8t
+CM_DEVICE int f8_slot(int kk) {
+  const int hf = kk >> 5, w = kk & 31;
+  const int h = (w >> 2) & 1, r = (w & 3) + 4 * (w >> 3);
+  return 32 * h + 16 * hf + r;
+}
+
+__global__ void attn_fp8_pack_kernel(AttnArgs a, int Hk, int Nkp, uint8_t* __restrict__ K8,
+                                     uint8_t* __restrict__ V8t) {
+  // thread = (b, kv head, 8-wide d chunk, key); keys fastest so V8t byte rows are coalesced
+  const long long total = (long long)a.B * Hk * 8 * Nkp;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int key = (int)(i % Nkp);
+  long long r = i / Nkp;
+  const int ch = (int)(r % 8);
+  r /= 8;
+  const int hh = (int)(r % Hk);
+  const int b = (int)(r / Hk);
+  uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+  int nk = a.Nk;
+  if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
+  if (key < nk && ch * 8 < a.d) {
+    kv = *reinterpret_cast<const uint4*>(a.k + (long long)b * a.k_sb + (long long)key * a.k_sn +
+                                         (long long)hh * a.k_sh + ch * 8);
+    vv = *reinterpret_cast<const uint4*>(a.v + (long long)b * a.v_sb + (long long)key * a.v_sn +
+                                         (long long)hh * a.v_sh + ch * 8);
+  }
+  float kf[8], vf[8];
+  unpack8(kv, kf);
+  unpack8(vv, vf);
+  const long long bh = (long long)b * Hk + hh;
+  *reinterpret_cast<uint2*>(K8 + (bh * Nkp + key) * 64 + ch * 8) =
+      make_uint2(f8x4(kf[0], kf[1], kf[2], kf[3]), f8x4(kf[4], kf[5], kf[6], kf[7]));
+  const uint32_t v0 = f8x4(vf[0], vf[1], vf[2], vf[3]), v1 = f8x4(vf[4], vf[5], vf[6], vf[7]);
+  const int slot = (key & ~63) + f8_slot(key & 63);
+  uint8_t* vt = V8t + (bh * 64 + ch * 8) * Nkp + slot;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    vt[(long long)e * Nkp] = (uint8_t)(v0 >> (8 * e));
+    vt[(long long)(e + 4) * Nkp] = (uint8_t)(v1 >> (8 * e));
+  }
+}
+
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8,
+                                                           const uint8_t* __restrict__ V8t) {
+  constexpr int THREADS = 64 * NW;
+  constexpr int QB = 32 * NW;
+  constexpr int TILE_B = KT * F8_KSTR;   // one 64-row fp8 tile in LDS
+  __shared__ __attribute__((aligned(16))) uint8_t Ks[TILE_B];
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[TILE_B];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hlf = lane >> 5, ql = lane & 31;
+  const int nqb = (a.Nq + QB - 1) / QB;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb, bh = bid / nqb;
+  const int h = bh % a.H, b = bh / a.H;
+  const int hk = a.group > 1 ? h / a.group : h;
+  const int q0 = qb * QB + wave * 32, q = q0 + ql;
+
+  int nk = a.Nk;
+  if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
+  int ntiles = (nk + KT - 1) / KT;
+  if (a.causal) ntiles = min(ntiles, (qb * QB + QB + KT - 1) / KT);
+
+  // Q8 fragment: lane holds Q[q][32*hlf .. +31] * scale*log2e as e4m3
+  i32x8_t qf;
+  {
+    const uint16_t* Qp = a.q + (long long)b * a.q_sb + (long long)h * a.q_sh + (long long)q * a.q_sn + 32 * hlf;
+    const float sc = a.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.Nq) v = *reinterpret_cast<const uint4*>(Qp + 8 * c);
+      float f[8];
+      unpack8(v, f);
+      qf[2 * c] = (int)f8x4(f[0] * sc, f[1] * sc, f[2] * sc, f[3] * sc);
+      qf[2 * c + 1] = (int)f8x4(f[4] * sc, f[5] * sc, f[6] * sc, f[7] * sc);
+    }
+  }
+  const uint8_t* Kg = K8 + ((long long)b * Hk + hk) * Nkp * 64;
+  const uint8_t* Vg = V8t + ((long long)b * Hk + hk) * 64 * Nkp;
+  // staging: 256 16-byte chunks per tile and operand (row = chunk >> 2, 4 chunks per row)
+  constexpr int LD = (KT * 4 + THREADS - 1) / THREADS;
+  uint4 kr[LD], vr[LD];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int c = tid + i * THREADS;
+      if (c < KT * 4) {
+        const int row = c >> 2, cc = c & 3;
+        kr[i] = *reinterpret_cast<const uint4*>(Kg + (long long)(t * KT + row) * 64 + cc * 16);
+        vr[i] = *reinterpret_cast<const uint4*>(Vg + (long long)row * Nkp + t * KT + cc * 16);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int c = tid + i * THREADS;
+      if (c < KT * 4) {
+        const int row = c >> 2, cc = c & 3;
+        *reinterpret_cast<uint4*>(Ks + row * F8_KSTR + cc * 16) = kr[i];
+        *reinterpret_cast<uint4*>(Vs + row * F8_KSTR + cc * 16) = vr[i];
+      }
+    }
+  };
+  if (ntiles > 0) { gload(0); lstore(); }
+  __syncthreads();
+
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = 0.f, l_run = 0.f;
+  constexpr float RESCALE_THR = 8.f;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = t + 1 < ntiles;
+    if (more) gload(t + 1);
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[hf][r] = -m_run;
+      const uint8_t* kp = Ks + (hf * 32 + ql) * F8_KSTR + 32 * hlf;
+      const uint4 k0 = *reinterpret_cast<const uint4*>(kp);
+      const uint4 k1 = *reinterpret_cast<const uint4*>(kp + 16);
+      const i32x8_t kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
+      sacc[hf] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, sacc[hf], 0, 0, 0, 127, 0, 127);
+    }
+    const int kbase = t * KT;
+    const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
+    if (need_mask) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + hf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hlf;
+          if (key >= nk || (a.causal && key > q)) sacc[hf][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (t == 0 || !__all(mx <= RESCALE_THR)) {
+      float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
+      if (!(delta > -1e30f)) delta = 0.f;
+      m_run += delta;
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[hf][r] -= delta;
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
+        sacc[hf][r] = pv;
+        rs += pv;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run += rs;
+    // P^T fragment: element j = sacc[j >> 4][j & 15]
+    i32x8_t pf;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        pf[4 * hf + c] = (int)f8x4(sacc[hf][4 * c], sacc[hf][4 * c + 1], sacc[hf][4 * c + 2], sacc[hf][4 * c + 3]);
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc) {
+      const uint8_t* vp = Vs + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
+      const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
+      const i32x8_t vf = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+      oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
+    }
+    __syncthreads();
+    if (more) {
+      lstore();
+      __syncthreads();
+    }
+  }
+  if (q < a.Nq) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    uint16_t* Op = a.o + (long long)b * a.o_sb + (long long)q * a.o_sn + (long long)h * a.o_sh;
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = 32 * dc + 8 * g4 + 4 * hlf;
+        uint2 w;
+        w.x = pack2(oacc[dc][4 * g4 + 0] * inv, oacc[dc][4 * g4 + 1] * inv);
+        w.y = pack2(oacc[dc][4 * g4 + 2] * inv, oacc[dc][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(Op + dd) = w;
+      }
+  }
+}
+
 }  // namespace
+
+long long attention_fp8_workspace(const AttnArgs& a, int Hk) {
+  const long long Nkp = (a.Nk + KT - 1) / KT * KT;
+  return 2LL * a.B * Hk * Nkp * 64;   // bytes: K8 + V8t
+}
+
+void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s) {
+  const int Nkp = (a.Nk + KT - 1) / KT * KT;
+  uint8_t* K8 = ws;
+  uint8_t* V8t = ws + (long long)a.B * Hk * Nkp * 64;
+  const long long total = (long long)a.B * Hk * 8 * Nkp;
+  hipLaunchKernelGGL(attn_fp8_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, Hk, Nkp, K8, V8t);
+  const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
+  if (blocks8 >= 1024) {
+    const int nqb = (a.Nq + 255) / 256;
+    hipLaunchKernelGGL(attn_fp8_kernel<8>, dim3(nqb * a.H * a.B), dim3(512), 0, s, a, Hk, Nkp, K8, V8t);
+  } else {
+    const int nqb = (a.Nq + 127) / 128;
+    hipLaunchKernelGGL(attn_fp8_kernel<4>, dim3(nqb * a.H * a.B), dim3(256), 0, s, a, Hk, Nkp, K8, V8t);
+  }
+}
 
 void launch_attention(const AttnArgs& a, hipStream_t s) {
   switch (a.d) {

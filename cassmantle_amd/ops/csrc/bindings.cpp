@@ -186,7 +186,13 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
     TORCH_CHECK(kv_lens->scalar_type() == at::kInt && kv_lens->is_cuda(), "kv_lens must be int32 on device");
     a.kv_lens = kv_lens->data_ptr<int>();
   }
-  (void)fp8;
+  if (fp8 && a.d == 64) {
+    // OCP e4m3 K/V packed per call (workspace from the caching allocator: graph-safe)
+    const int Hk = (int)k.size(2);
+    auto ws = at::empty({attention_fp8_workspace(a, Hk)}, q.options().dtype(at::kByte));
+    launch_attention_fp8(a, Hk, ws.data_ptr<uint8_t>(), cur_stream());
+    return;
+  }
   launch_attention(a, cur_stream());
 }
 

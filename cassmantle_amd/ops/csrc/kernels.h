@@ -47,6 +47,9 @@ struct AttnArgs {
   int group = 1;                  // query heads per K/V head (GQA)
 };
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// fp8 (OCP e4m3) attention for head dim 64: ws = attention_fp8_workspace bytes (K8 + V8t)
+long long attention_fp8_workspace(const AttnArgs& a, int Hk);
+void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
 
 // norms
 void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,

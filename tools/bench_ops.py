@@ -98,6 +98,12 @@ def bench_attn(it):
         ops.set_mode("hip")
         fl = 4.0 * B * Hh * Nq * Nk * d
         emit("attention", [B, Nq, Nk, Hh, d], fl, t1, t2)
+    # SDXL shapes (head dim 64): bf16 kernel vs the fp8 (OCP e4m3) kernel (BASELINE config 4)
+    for B, Nq, Nk, Hh in [(2, 4096, 4096, 10), (2, 1024, 1024, 20), (2, 4096, 77, 10), (2, 1024, 77, 20)]:
+        q, k, v = rnd(B, Nq, Hh, 64), rnd(B, Nk, Hh, 64), rnd(B, Nk, Hh, 64)
+        t8 = timeit(lambda: ops.attention(q, k, v, fp8="force"), it)
+        t16 = timeit(lambda: ops.attention(q, k, v), it)
+        emit("attention_fp8_vs_bf16", [B, Nq, Nk, Hh, 64], 4.0 * B * Hh * Nq * Nk * 64, t8, t16)
 
 
 def bench_norm(it):
