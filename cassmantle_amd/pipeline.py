@@ -105,6 +105,9 @@ class StableDiffusion:
         self.vae = VAEDecoder(spec.vae, seed=seed, dtype=dtype).to(self.device).eval()
         self._states: Dict[tuple, _StepState] = {}
         self.timings: Dict[str, float] = {}
+        # generation runs on its own stream (never the legacy default stream), so a serving
+        # process can overlap it with the scorer's high-priority stream (BASELINE config 5)
+        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
 
     @property
     def latent_size(self) -> int:
@@ -191,13 +194,21 @@ class StableDiffusion:
     def generate_tensor(self, prompts: Sequence[str], negative: str, seeds: Sequence[int],
                         steps: Optional[int] = None, guidance: Optional[float] = None,
                         scheduler: Optional[str] = None) -> torch.Tensor:
-        """-> uint8 [B, H, W, 3] on device."""
+        """-> uint8 [B, H, W, 3] on device (ordered before the caller's current stream)."""
         plan = make_plan(scheduler or self.spec.scheduler, steps or self.spec.steps,
                          self.spec.guidance if guidance is None else guidance)
-        ctx, added = self.encode_prompt(prompts, negative)
-        x0 = self.init_latents(seeds, plan)
-        x = self.denoise(ctx, x0, plan, added)
-        return self.vae.decode_uint8(x.to(self.dtype))
+        caller = torch.cuda.current_stream(self.device) if self.stream is not None else None
+        with (torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()):
+            if caller is not None:
+                self.stream.wait_stream(caller)     # inputs the caller produced
+            ctx, added = self.encode_prompt(prompts, negative)
+            x0 = self.init_latents(seeds, plan)
+            x = self.denoise(ctx, x0, plan, added)
+            img = self.vae.decode_uint8(x.to(self.dtype))
+        if caller is not None:
+            caller.wait_stream(self.stream)
+            img.record_stream(caller)
+        return img
 
     def generate(self, prompts: Sequence[str], negative: str, seeds: Sequence[int], **kw) -> List[np.ndarray]:
         img = self.generate_tensor(prompts, negative, seeds, **kw)

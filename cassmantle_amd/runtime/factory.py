@@ -25,7 +25,8 @@ def build_scorer(cfg: Config, device: Optional[str] = None):
         backend = WordVectorBackend(device=dev, dtype=torch.bfloat16 if dev.startswith("cuda") else torch.float32)
     else:
         from ..scoring.encoder import EncoderBackend
-        backend = EncoderBackend(device=dev)
+        # high-priority stream: guess scoring is dispatched ahead of queued denoise kernels
+        backend = EncoderBackend(device=dev, stream_priority=-1 if dev.startswith("cuda") else None)
     return BatchingScorer(backend, cfg.game.min_score, window_ms=cfg.model.scorer_batch_window_ms)
 
 

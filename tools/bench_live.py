@@ -1,0 +1,153 @@
+"""BASELINE config 5: a live round — image generation and streaming guess scoring overlapped.
+
+Each rank (one per GPU, ``torchrun`` for N > 1) owns its rooms' content generation AND the
+guess scoring of its rooms' players:
+
+* a generation thread replays the hipGraph-captured SD-1.5 denoise loop back to back
+  (batch 4 images per room, 512², 50 PNDM steps) on the default stream;
+* an asyncio loop runs ``players / world`` simulated players per rank; each submits its two
+  mask guesses, waits for the scores, "thinks" for a random 0.5–1.5 × ``--think-ms`` and
+  repeats.  Requests go through the micro-batching scorer (``scoring.batcher``), whose MiniLM
+  embed + cosine runs on a HIGH-PRIORITY stream (``EncoderBackend(stream_priority=-1)``) so
+  scoring kernels are dispatched ahead of queued denoise kernels.
+
+Phases: ``--idle-s`` seconds of scoring alone (latency floor), then ``--seconds`` with both.
+Rank 0 prints one JSON line: whole-job images/s during the overlapped phase, p50/p99 guess
+latency idle vs under load (max over ranks), and requests served.
+
+    python tools/bench_live.py --seconds 30
+    torchrun --nproc-per-node 8 tools/bench_live.py --players 64
+"""
+import argparse
+import asyncio
+import json
+import os
+import random
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--players", type=int, default=64, help="total over all ranks")
+    ap.add_argument("--seconds", type=float, default=30.0)
+    ap.add_argument("--idle-s", type=float, default=8.0)
+    ap.add_argument("--think-ms", type=float, default=250.0)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--model", default="sd15")
+    ap.add_argument("--priority", type=int, default=-1, help="scorer stream priority (lower = higher)")
+    ap.add_argument("--no-priority", action="store_true",
+                    help="A/B: score on a normal-priority side stream.  (Scoring on the legacy default "
+                         "stream while the generation thread replays graphs stalled the process on "
+                         "MI355X in two runs; the serving stack never does that.)")
+    ap.add_argument("--window-ms", type=float, default=1.0)
+    return ap.parse_args()
+
+
+WORDS = ("lantern river tower garden mirror orchard ancient crimson hollow silent glowing ember shadow "
+         "velvet frozen radiant amber comet glacier harbor meadow falcon violin").split()
+
+
+async def player(scorer, rng, stop_at, lat, think_ms):
+    while time.perf_counter() < stop_at:
+        pairs = [(rng.choice(WORDS), rng.choice(WORDS)) for _ in range(2)]
+        t0 = time.perf_counter()
+        await scorer.score(pairs)
+        lat.append((time.perf_counter() - t0) * 1e3)
+        await asyncio.sleep(think_ms / 1e3 * rng.uniform(0.5, 1.5))
+
+
+async def run_players(scorer, n, seconds, think_ms, seed):
+    lat = []
+    stop_at = time.perf_counter() + seconds
+    rngs = [random.Random(seed * 1000 + i) for i in range(n)]
+    await asyncio.gather(*(player(scorer, r, stop_at, lat, think_ms) for r in rngs))
+    return lat
+
+
+def main():
+    a = parse()
+    from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
+    from cassmantle_amd.parallel import dist as cdist
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    from cassmantle_amd.scoring.batcher import BatchingScorer
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+
+    ctx = cdist.init_from_env()
+    rank, world, dev = ctx.rank, ctx.world_size, ctx.device
+    n_players = a.players // world + (1 if rank < a.players % world else 0)
+    sd = StableDiffusion(SPECS[a.model], device=dev, seed=0)
+    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
+    scorer = BatchingScorer(backend, 0.01, window_ms=a.window_ms)
+    gen = SyntheticPromptGenerator(salt=rank)
+    seeds_txt, styles = load_seeds(), load_styles()
+    neg = "blurry, distorted, fake, abstract, negative"
+
+    def prompts(step):
+        return [image_prompt(styles[(step + j) % len(styles)],
+                             gen.generate(seeds_txt[(rank + step + j) % len(seeds_txt)] + "\n", True),
+                             "A {style} style piece depicting the following: ") for j in range(a.batch)]
+
+    # warm everything (graph capture, allocator, scorer shapes)
+    sd.generate_tensor(prompts(0), neg, list(range(a.batch))).cpu()
+    asyncio.run(run_players(scorer, min(n_players, 4), 1.0, a.think_ms, rank + 99))
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+
+    idle = asyncio.run(run_players(scorer, n_players, a.idle_s, a.think_ms, rank))
+
+    done = {"images": 0}
+    stop = threading.Event()
+
+    def gen_loop():
+        step = 1
+        while not stop.is_set():
+            img = sd.generate_tensor(prompts(step), neg, [rank * 10000 + step * 10 + j for j in range(a.batch)])
+            img.cpu()                       # completes this batch (blocks this thread only)
+            done["images"] += a.batch
+            step += 1
+
+    if world > 1:
+        torch.distributed.barrier()
+    th = threading.Thread(target=gen_loop, daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    load = asyncio.run(run_players(scorer, n_players, a.seconds, a.think_ms, rank + 7))
+    imgs_at_stop = done["images"]
+    elapsed = time.perf_counter() - t0
+    stop.set()
+    th.join()
+
+    def pct(x, q):
+        return float(np.percentile(np.asarray(x), q)) if x else float("nan")
+
+    stats = torch.tensor([imgs_at_stop / elapsed, pct(idle, 50), pct(idle, 99), pct(load, 50), pct(load, 99),
+                          float(len(load))], dtype=torch.float64, device=dev)
+    if world > 1:
+        allv = [torch.zeros_like(stats) for _ in range(world)]
+        torch.distributed.all_gather(allv, stats)
+        m = torch.stack(allv)
+        agg = [m[:, 0].sum(), m[:, 1].max(), m[:, 2].max(), m[:, 3].max(), m[:, 4].max(), m[:, 5].sum()]
+        stats = torch.stack(agg)
+    if rank == 0:
+        s = [float(x) for x in stats.tolist()]
+        print(json.dumps({
+            "metric": "live round: images/s with overlapped streaming guess scoring (BASELINE config 5)",
+            "images_per_s": round(s[0], 3), "n_gpus": world, "players": a.players,
+            "think_ms": a.think_ms, "idle_p50_ms": round(s[1], 3), "idle_p99_ms": round(s[2], 3),
+            "load_p50_ms": round(s[3], 3), "load_p99_ms": round(s[4], 3), "requests": int(s[5]),
+            "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
+            "config": {"model": a.model, "batch_per_room": a.batch, "graphs": bool(sd.use_graphs)}}), flush=True)
+    cdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()
