@@ -48,6 +48,16 @@ CM_DEVICE void glds16(const void* src, uint4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
+// buffer-resource LDS-DMA: 16 B per lane to lds_wave_base + 16*lane, source rsrc + voff + soff
+// (device-only helper: the address-space cast must not appear in a host-instantiated body)
+CM_DEVICE void blds16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+CM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
 template <int N>
 CM_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -96,7 +106,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
 __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
@@ -184,6 +194,44 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
   const int Wv = p.upsample ? 2 * p.IW : p.IW;
   const bool kfull = (p.K % BK) == 0;     // no k bound checks needed
 
+  // ---- BUF: LDS-DMA through buffer resources (buffer_load_dwordx4 ... lds).  The per-lane
+  // part of every source address is a constant 32-bit voffset computed here once; the per-k-tile
+  // part (k0, or the conv tap offset) is a wave-uniform SGPR soffset, so staging a k-tile costs
+  // no VALU address math (the global_load_lds path spent ~4 VALU + 3.6 SALU per MFMA on it,
+  // rocprof PMC).  Invalid rows / conv padding use voffset 0x80000000 >= num_records: the
+  // buffer unit returns zeros (no zero page, no per-tile select).  Conv tap validity is a
+  // per-lane bitmask over the ksize^2 taps.
+  __amdgpu_buffer_rsrc_t rsA, rsW;
+  int a_vo[BUF ? AR : 1], a_mask[BUF ? AR : 1], w_vo[BUF ? WR : 1];
+  if constexpr (BUF) {
+    constexpr int OOB = (int)0x80000000;
+    long long biasA = 0;   // bytes: lowest pixel offset a conv tap can address is -bias
+    if constexpr (CONV == 2) biasA = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
+    const long long a_bytes = CONV ? (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2
+                                   : ((long long)(p.M - 1) * p.lda + p.K) * 2;
+    rsA = make_rsrc((const char*)A - biasA, a_bytes + biasA);
+    const long long w_bytes = ((long long)(p.Nw - 1) * ldw + p.K) * 2;
+    rsW = make_rsrc(W, w_bytes);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      if constexpr (CONV == 0) {
+        a_vo[i] = a_ok[i] ? (int)(a_off[i] * 2) : OOB;
+        a_mask[i] = 0;
+      } else {
+        a_vo[i] = a_ok[i] ? (int)(a_off[i] * 2 + biasA) : OOB;
+        int mk = 0;
+        for (int ky = 0; ky < p.ksize; ++ky)
+          for (int kx = 0; kx < p.ksize; ++kx) {
+            const int iy = cy_[i] + ky, ix = cx_[i] + kx;
+            if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) mk |= 1 << (ky * p.ksize + kx);
+          }
+        a_mask[i] = a_ok[i] ? mk : 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) w_vo[i] = w_row[i] >= 0 ? (int)(w_off[i] * 2) : OOB;
+  }
+
   // wave-uniform conv tap state for CONV >= 2 (Cin % 64 == 0: a k-tile is 64 channels of one
   // tap), advanced incrementally as the k-tiles are staged in order
   int t_ci = 0, t_kx = 0, t_ky = 0;
@@ -207,6 +255,26 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
     const bool kin = kfull || (k0 + BK <= p.K);   // whole tile inside K (uniform)
     uint4* As = smem + buf * TILE;
     uint4* Ws = As + BM * 8;
+    if constexpr (BUF) {                           // (host guarantees K % BK == 0)
+      int soffA = k0 * 2, tap = 0;
+      if constexpr (CONV == 2) {
+        soffA = ((t_ky * p.IW + t_kx) * p.Cin + t_ci) * 2;
+        tap = t_ky * p.ksize + t_kx;
+      }
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        int vo = a_vo[i];
+        if constexpr (CONV == 2) vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
+        blds16(rsA, As + (32 * i + 8 * wave) * 8, vo, soffA);
+      }
+#pragma unroll
+      for (int i = 0; i < WR; ++i) {
+        if (32 * i + 8 * wave < BN)
+          blds16(rsW, Ws + (32 * i + 8 * wave) * 8, w_vo[i], k0 * 2);
+      }
+      if constexpr (CONV >= 2) tap_next();
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const void* src = zp;
@@ -256,23 +324,25 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
 
   const int fr = lane & 15;      // fragment row within 16
   const int fq = lane >> 4;      // k-chunk within a 32-k step
+  // fragment read addresses are loop-invariant: rows 16*i + r0 share the swizzle of r0
+  // ((r0 + 16 i) >> 1) & 7 == (r0 >> 1) & 7), so each k-step needs ONE lane offset per operand
+  // and the per-fragment / per-buffer parts are ds_read immediates
+  const int w_r0 = wn * (BN / WN) + fr, a_r0 = wm * (BM / WM) + fr;
+  int w_rd[2], a_rd[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    w_rd[ks] = BM * 8 + w_r0 * 8 + swz(w_r0, ks * 4 + fq);
+    a_rd[ks] = a_r0 * 8 + swz(a_r0, ks * 4 + fq);
+  }
   auto compute = [&](int buf) {
-    const uint4* As = smem + buf * TILE;
-    const uint4* Ws = As + BM * 8;
+    const uint4* Bs = smem + buf * TILE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 4 + fq;
       bf16x8_t wf[TI], af[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wn * (BN / WN) + 16 * i + fr;
-        wf[i] = as_bf16x8(Ws[r * 8 + swz(r, ch)]);
-      }
+      for (int i = 0; i < TI; ++i) wf[i] = as_bf16x8(Bs[w_rd[ks] + 16 * 8 * i]);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wm * (BM / WM) + 16 * j + fr;
-        af[j] = as_bf16x8(As[r * 8 + swz(r, ch)]);
-      }
+      for (int j = 0; j < TJ; ++j) af[j] = as_bf16x8(Bs[a_rd[ks] + 16 * 8 * j]);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -291,10 +361,15 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __r
   if constexpr (STAGES == 2) {
     if (nk > 0) stage(kt0, 0);
     __syncthreads();                       // drains the DMA (vmcnt(0)) and publishes the tile
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) stage(kt0 + t + 1, (t + 1) & 1);
-      compute(t & 1);
+    // unrolled by two so the LDS buffer of every stage/compute is a compile-time offset
+    for (int t = 0; t < nk; t += 2) {
+      if (t + 1 < nk) stage(kt0 + t + 1, 1);
+      compute(0);
       __syncthreads();                     // next tile landed and everyone is done with this one
+      if (t + 1 >= nk) break;
+      if (t + 2 < nk) stage(kt0 + t + 2, 0);
+      compute(1);
+      __syncthreads();
     }
   } else {
     if (nk > 0) stage(kt0, 0);
@@ -488,23 +563,25 @@ int stages_pref() {
   return g_stages_override;
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
 void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
   const int split = (ws != nullptr && p.split > 1) ? p.split : 1;
   dim3 grid(nN * nM, split, p.batch);
   constexpr size_t lds = (size_t)STAGES * (BM + BN) * BK * 2;
+  // (the kernel is named once, outside any lambda: a kernel template referenced only from a
+  // lambda inside this function template was left uninstantiated by hipcc)
+  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
-    static const bool once = [] {
-      (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      return true;
-    }();
-    (void)once;
+    static bool once = false;
+    if (!once) {
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      once = true;
+    }
   }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES>), grid, dim3(THREADS), lds, s, p, ws);
+  hipLaunchKernelGGL(kfn, grid, dim3(THREADS), lds, s, p, ws);
   if (split > 1) {
     const long long nq = (long long)p.M * (p.N / 4);
     const long long nb = (nq + 255) / 256;
@@ -513,17 +590,17 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, bool BUF>
 void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
   // STAGES=3 (counted vmcnt, one block/CU) measured 1.3-1.7x SLOWER than 2 stages at 2
   // blocks/CU on every SD shape (profiles/r1_ops_stages_ab.txt); define CASSMANTLE_GEMM_3STAGE
   // to compile it for experiments.
 #ifdef CASSMANTLE_GEMM_3STAGE
-  if constexpr (BN % 32 == 0) {
-    if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3>(p, ws, s);
+  if constexpr (BN % 32 == 0 && !BUF) {
+    if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3, false>(p, ws, s);
   }
 #endif
-  launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2>(p, ws, s);
+  launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2, BUF>(p, ws, s);
 }
 
 // Tile menu (all 4 waves, 2 blocks per CU by LDS):
@@ -533,22 +610,40 @@ constexpr TileCfg kTiles[5] = {{128, 128, 1.00f}, {128, 160, 1.02f}, {256, 64, 0
                                {256, 16, 0.25f}};
 constexpr int kSlots = 512;   // resident blocks: 256 CUs x 2
 
-template <int CONV, bool OUTF32>
+template <int CONV, bool OUTF32, bool BUF>
 void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
   switch (p.cfg) {
-    case 1: launch_st<128, 160, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
-    case 2: launch_st<256, 64, 4, 1, CONV, false, OUTF32>(p, ws, s); break;
-    case 3: launch_st<128, 64, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
-    case 4: launch_st<256, 16, 4, 1, CONV, false, OUTF32>(p, ws, s); break;
-    default: launch_st<128, 128, 2, 2, CONV, false, OUTF32>(p, ws, s); break;
+    case 1: launch_st<128, 160, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
+    case 2: launch_st<256, 64, 4, 1, CONV, false, OUTF32, BUF>(p, ws, s); break;
+    case 3: launch_st<128, 64, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
+    case 4: launch_st<256, 16, 4, 1, CONV, false, OUTF32, BUF>(p, ws, s); break;
+    default: launch_st<128, 128, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
   }
 }
 
-template <int CONV>
+template <int CONV, bool BUF>
 void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
-  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) launch_st<128, 128, 2, 2, CONV, true, false>(p, ws, s);
-  else if (p.out_f32) launch_cfg<CONV, true>(p, ws, s);
-  else launch_cfg<CONV, false>(p, ws, s);
+  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);
+  else if (p.out_f32) launch_cfg<CONV, true, BUF>(p, ws, s);
+  else launch_cfg<CONV, false, BUF>(p, ws, s);
+}
+
+// buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
+// 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
+bool buf_ok(const GemmArgs& p) {
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("CASSMANTLE_GEMM_BUF");
+    force = e ? atoi(e) : 1;
+  }
+  if (!force || p.K % BK != 0) return false;
+  const long long ldw = p.ldw ? p.ldw : p.K;
+  const long long lim = (1LL << 31) - 1;
+  if (((long long)(p.Nw - 1) * ldw + p.K) * 2 > lim) return false;
+  if (!p.conv) return ((long long)(p.M - 1) * p.lda + p.K) * 2 <= lim;
+  if (p.upsample || p.Cin % 64 != 0) return false;
+  const long long bias = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
+  return (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2 + bias <= lim;
 }
 
 }  // namespace
@@ -604,11 +699,15 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
       hipLaunchKernelGGL(gemm_simt_kernel<0>, grid, dim3(256), 0, s, p);
     return;
   }
-  if (!p.conv) launch_tiles<0>(p, ws, s);
-  else if (p.Cin % 64 == 0) {
-    if (p.upsample) launch_tiles<3>(p, ws, s);
-    else launch_tiles<2>(p, ws, s);
+  const bool buf = buf_ok(p);
+  if (!p.conv) {
+    if (buf) launch_tiles<0, true>(p, ws, s);
+    else launch_tiles<0, false>(p, ws, s);
+  } else if (p.Cin % 64 == 0) {
+    if (p.upsample) launch_tiles<3, false>(p, ws, s);
+    else if (buf) launch_tiles<2, true>(p, ws, s);
+    else launch_tiles<2, false>(p, ws, s);
   } else {
-    launch_tiles<1>(p, ws, s);
+    launch_tiles<1, false>(p, ws, s);
   }
 }
