@@ -1,513 +1,47 @@
-// MFMA bf16 GEMM / implicit-GEMM convolution with fused epilogues.
-//
-//   D[n][m] = sum_k W[n][k] * A[m][k]          (computed transposed so each lane owns 4
-//   C[m][n] = act(alpha*D + bias[n] + cb[b][n])  consecutive output channels of one row ->
-//             (+ residual[m][n])                 8-byte NHWC stores)
-//
-// * A is either a row-major activation matrix (linear layers, 1x1 convs) or an NHWC image read
-//   through an implicit im2col (3x3 convs, stride-2 downsamplers, and the nearest-2x upsample
-//   fused into the address generation: the upsampled tensor never exists).
-// * W rows are K-contiguous ([Cout][kh][kw][Cin] for convs), so both operands are read from
-//   LDS as 16-byte k-chunks: mfma_f32_16x16x32_bf16 fragments straight from ds_read_b128.
-// * Global -> LDS by LDS-DMA (global_load_lds_dwordx4, cdna_hip_programming.md §5): no VGPR
-//   staging, no ds_write; each wave-instruction fills 8 rows x 128 B.  Out-of-range rows and
-//   conv padding point their lane at a 16-byte zero page.
-//   - STAGES=2: the next k-tile's DMA is issued before the current tile's MFMAs; one
-//     __syncthreads (= vmcnt(0) + barrier) per k-tile.
-//   - STAGES=3: two tiles in flight; a counted `s_waitcnt vmcnt(N)` retires only the tile about
-//     to be read and a raw s_barrier publishes it, so one DMA stays in flight across every
-//     barrier ("Pipelining across barriers", guide §5).
-// * LDS rows are 128 B; logical chunk c of row r lives in slot c ^ ((r >> 1) & 7).  The DMA
-//   image is lane-linear, so the swizzle is applied on the SOURCE address (rule 21) and the
-//   same XOR on the ds_read; each 16-lane ds_read_b128 group then hits 16 distinct bank slots.
-// * Tiles (BM x BN x 64, 4 waves as WM x WN): 128x128 (2x2), 256x64 (4x1) for N = 64 (mod
-//   128), 256x16 (4x1) for the 3/4-channel conv_out layers.
-// * Split-K: grids that cannot fill the 256 CUs (the 16x16 / 8x8 UNet levels: M = 2048 / 512
-//   with K = 11520) split the k-tiles over blockIdx.y; fp32 partial slabs are summed by a
-//   second kernel that applies the epilogue (cheaper than a sub-occupied chip).
-// * GEGLU (transformer FF): W tile rows interleave 16-row value/gate blocks, so each lane
-//   holds h and g of the same output column and computes h * gelu(g) in registers.
-// * Block ids are remapped XCD-aware so tiles that share an A panel run on one XCD's L2.
+// MFMA GEMM / implicit-GEMM conv: tile planner and dispatch (kernels: gemm_impl.h, instantiated
+// per A-operand mode in gemm_c*.hip).
 #include <stdlib.h>
 
 #include "common.h"
 #include "kernels.h"
 
-__device__ uint4 g_zero_page[4];   // zero-initialised; source of padded / out-of-range chunks
+void gemm_c0_buf_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_c0_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_c1_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_c2_buf_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_c3_launch(const GemmArgs& p, float* ws, hipStream_t s);
 
 namespace {
 
 constexpr int BK = 64;
-constexpr int THREADS = 256;
 
-CM_DEVICE int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// Tile menu.  4 waves, 2 blocks per CU by LDS, 2 stages:
+//   0: 128x128 (2x2)   1: 128x160 (2x2, wave 80x64)   2: 256x64 (4x1)   3: 128x64 (2x2)   4: 256x16 (4x1)
+// 8 waves, 1 block per CU, 3-stage ring:
+//   5: 256x160 (4x2, wave 64x80)   6: 256x128 (4x2, wave 64x64)
+struct TileCfg { int BM, BN; float eff; int slots; };
+constexpr int kNumTiles = 7;
+constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f, 512}, {256, 64, 0.95f, 512},
+                                       {128, 64, 0.80f, 512},  {256, 16, 0.25f, 512},  {256, 160, 1.02f, 256},
+                                       {256, 128, 1.00f, 256}};
 
-typedef __attribute__((address_space(3))) void lds_void;
-
-CM_DEVICE void glds16(const void* src, uint4* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
-}
-
-// buffer-resource LDS-DMA: 16 B per lane to lds_wave_base + 16*lane, source rsrc + voff + soff
-// (device-only helper: the address-space cast must not appear in a host-instantiated body)
-CM_DEVICE void blds16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, voff, soff, 0, 0);
-}
-
-CM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-
-template <int N>
-CM_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-CM_DEVICE void add4(float* o, uint2 v) {
-  o[0] += bf2f(v.x & 0xffff); o[1] += bf2f(v.x >> 16); o[2] += bf2f(v.y & 0xffff); o[3] += bf2f(v.y >> 16);
-}
-
-// epilogue for 4 consecutive output columns n..n+3 of row m (raw accumulators in o)
-template <bool OUTF32>
-CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
-  const int hw = p.Ho * p.Wo;
-  const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
-  const long long cbs = p.ldcb ? p.ldcb : p.N;
-  const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (cbs % 4 == 0);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
-  if (full) {
-    if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
-    if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
-    if (p.act != ACT_NONE) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
-    }
-    if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
-    if constexpr (OUTF32) {
-      float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-      *reinterpret_cast<float4*>(C) = make_float4(o[0], o[1], o[2], o[3]);
-    } else {
-      uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-      *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-    }
-  } else {   // ragged N (3-channel conv_out): element-wise tail
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (n + r >= p.N) break;
-      float v = o[r];
-      if (p.bias) v += bf2f(p.bias[n + r]);
-      if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * cbs + n + r]);
-      v = apply_act(v, p.act);
-      if (p.residual) v += bf2f(p.residual[(long long)m * p.ldc + n + r]);
-      if constexpr (OUTF32)
-        reinterpret_cast<float*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = v;
-      else
-        reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = f2bf(v);
-    }
+// buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
+// 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
+bool buf_ok(const GemmArgs& p) {
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("CASSMANTLE_GEMM_BUF");
+    force = e ? atoi(e) : 1;
   }
-}
-
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
-__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-  constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
-  static_assert(WM * WN == 4, "4 waves");
-  constexpr int TI = BN / WN / 16;         // n-subtiles per wave
-  constexpr int TJ = BM / WM / 16;         // m-subtiles per wave
-  static_assert(!GEGLU || (TI % 2 == 0), "geglu pairs");
-  constexpr int AR = BM / 32;              // A DMA rounds (32 rows each, 8 per wave)
-  constexpr int WR = (BN + 31) / 32;       // W DMA rounds
-  static_assert(STAGES == 2 || (STAGES == 3 && BN % 32 == 0), "counted waits need equal DMA per wave");
-  constexpr int NPT = AR + WR;             // DMA instructions per wave per k-tile
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave % WM, wn = wave / WM;
-
-  const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
-  const int nM = (p.M + BM - 1) / BM;
-  const int lin = xcd_remap(blockIdx.x, nN * nM);
-  const int tn = lin % nN, tm = lin / nN;
-  const int batch = blockIdx.z;
-  const int m0 = tm * BM;
-  const int n0 = GEGLU ? tn * (BN / 2) : tn * BN;   // output-column origin
-
-  const uint16_t* __restrict__ A = p.A + (long long)batch * p.sA;
-  const uint16_t* __restrict__ W = p.W + (long long)batch * p.sW;
-  const int ldw = p.ldw ? p.ldw : p.K;
-  const void* zp = (const void*)g_zero_page;
-
-  // ---- this lane's DMA rows: round i covers rows 32i + 8*wave + (lane>>3), slot lane&7
-  const int slot = lane & 7;
-  const int rsub = 8 * wave + (lane >> 3);
-  // Per-row state is computed ONCE; the per-k-tile address work is then a few VALU ops per DMA
-  // (the first version recomputed divisions per tile and was issue-bound on SALU/VALU:
-  // 15 SALU + 9 VALU per MFMA in the rocprof counters).
-  int a_chunk[AR];
-  long long a_off[AR];       // plain: row*lda + chunk*8 ; conv: element offset of pixel (b,cy,cx) + chunk*8
-  int cy_[AR], cx_[AR], cbh_[AR];
-  bool a_ok[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int r = 32 * i + rsub;
-    const int row = m0 + r;
-    a_chunk[i] = slot ^ ((r >> 1) & 7);
-    a_ok[i] = row < p.M;
-    if constexpr (CONV == 0) {
-      a_off[i] = (long long)row * p.lda + a_chunk[i] * 8;
-    } else {
-      const int m = a_ok[i] ? row : 0;
-      const int hw = p.Ho * p.Wo;
-      const int b = m / hw;
-      const int rr = m - b * hw;
-      const int oy = rr / p.Wo;
-      const int ox = rr - oy * p.Wo;
-      cy_[i] = oy * p.stride - p.pad;
-      cx_[i] = ox * p.stride - p.pad;
-      cbh_[i] = b * p.IH;
-      a_off[i] = (((long long)b * p.IH + cy_[i]) * p.IW + cx_[i]) * p.Cin + a_chunk[i] * 8;
-      if (!a_ok[i]) cy_[i] = -(1 << 28);   // never in bounds
-    }
-  }
-  int w_row[WR], w_chunk[WR];
-#pragma unroll
-  for (int i = 0; i < WR; ++i) {
-    const int r = 32 * i + rsub;
-    w_chunk[i] = slot ^ ((r >> 1) & 7);
-    int gr = -1;
-    if (r < BN) {
-      if constexpr (GEGLU) {
-        const int blk = r >> 4, within = r & 15;
-        const int nout = n0 + (blk >> 1) * 16 + within;
-        gr = (nout < p.N) ? ((blk & 1) ? p.N + nout : nout) : -1;
-      } else {
-        const int n = n0 + r;
-        gr = n < p.Nw ? n : -1;
-      }
-    }
-    w_row[i] = gr;
-  }
-  long long w_off[WR];
-#pragma unroll
-  for (int i = 0; i < WR; ++i) w_off[i] = (long long)(w_row[i] < 0 ? 0 : w_row[i]) * ldw + w_chunk[i] * 8;
-  const int Hv = p.upsample ? 2 * p.IH : p.IH;
-  const int Wv = p.upsample ? 2 * p.IW : p.IW;
-  const bool kfull = (p.K % BK) == 0;     // no k bound checks needed
-
-  // ---- BUF: LDS-DMA through buffer resources (buffer_load_dwordx4 ... lds).  The per-lane
-  // part of every source address is a constant 32-bit voffset computed here once; the per-k-tile
-  // part (k0, or the conv tap offset) is a wave-uniform SGPR soffset, so staging a k-tile costs
-  // no VALU address math (the global_load_lds path spent ~4 VALU + 3.6 SALU per MFMA on it,
-  // rocprof PMC).  Invalid rows / conv padding use voffset 0x80000000 >= num_records: the
-  // buffer unit returns zeros (no zero page, no per-tile select).  Conv tap validity is a
-  // per-lane bitmask over the ksize^2 taps.
-  __amdgpu_buffer_rsrc_t rsA, rsW;
-  int a_vo[BUF ? AR : 1], a_mask[BUF ? AR : 1], w_vo[BUF ? WR : 1];
-  if constexpr (BUF) {
-    constexpr int OOB = (int)0x80000000;
-    long long biasA = 0;   // bytes: lowest pixel offset a conv tap can address is -bias
-    if constexpr (CONV == 2) biasA = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
-    const long long a_bytes = CONV ? (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2
-                                   : ((long long)(p.M - 1) * p.lda + p.K) * 2;
-    rsA = make_rsrc((const char*)A - biasA, a_bytes + biasA);
-    const long long w_bytes = ((long long)(p.Nw - 1) * ldw + p.K) * 2;
-    rsW = make_rsrc(W, w_bytes);
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      if constexpr (CONV == 0) {
-        a_vo[i] = a_ok[i] ? (int)(a_off[i] * 2) : OOB;
-        a_mask[i] = 0;
-      } else {
-        a_vo[i] = a_ok[i] ? (int)(a_off[i] * 2 + biasA) : OOB;
-        int mk = 0;
-        for (int ky = 0; ky < p.ksize; ++ky)
-          for (int kx = 0; kx < p.ksize; ++kx) {
-            const int iy = cy_[i] + ky, ix = cx_[i] + kx;
-            if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) mk |= 1 << (ky * p.ksize + kx);
-          }
-        a_mask[i] = a_ok[i] ? mk : 0;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < WR; ++i) w_vo[i] = w_row[i] >= 0 ? (int)(w_off[i] * 2) : OOB;
-  }
-
-  // wave-uniform conv tap state for CONV >= 2 (Cin % 64 == 0: a k-tile is 64 channels of one
-  // tap), advanced incrementally as the k-tiles are staged in order
-  int t_ci = 0, t_kx = 0, t_ky = 0;
-  auto tap_init = [&](int kt) {
-    const int k0 = kt * BK;
-    const int tap = k0 / p.Cin;
-    t_ci = k0 - tap * p.Cin;
-    t_ky = tap / p.ksize;
-    t_kx = tap - t_ky * p.ksize;
-  };
-  auto tap_next = [&]() {
-    t_ci += BK;
-    if (t_ci == p.Cin) {
-      t_ci = 0;
-      if (++t_kx == p.ksize) { t_kx = 0; ++t_ky; }
-    }
-  };
-
-  auto stage = [&](int kt, int buf) {
-    const int k0 = kt * BK;
-    const bool kin = kfull || (k0 + BK <= p.K);   // whole tile inside K (uniform)
-    uint4* As = smem + buf * TILE;
-    uint4* Ws = As + BM * 8;
-    if constexpr (BUF) {                           // (host guarantees K % BK == 0)
-      int soffA = k0 * 2, tap = 0;
-      if constexpr (CONV == 2) {
-        soffA = ((t_ky * p.IW + t_kx) * p.Cin + t_ci) * 2;
-        tap = t_ky * p.ksize + t_kx;
-      }
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        int vo = a_vo[i];
-        if constexpr (CONV == 2) vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
-        blds16(rsA, As + (32 * i + 8 * wave) * 8, vo, soffA);
-      }
-#pragma unroll
-      for (int i = 0; i < WR; ++i) {
-        if (32 * i + 8 * wave < BN)
-          blds16(rsW, Ws + (32 * i + 8 * wave) * 8, w_vo[i], k0 * 2);
-      }
-      if constexpr (CONV >= 2) tap_next();
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const void* src = zp;
-      if constexpr (CONV == 0) {
-        if (a_ok[i] && (kin || k0 + a_chunk[i] * 8 < p.K)) src = A + a_off[i] + k0;
-      } else if constexpr (CONV == 1) {            // general (Cin % 8): per-lane tap decode
-        const int k = k0 + a_chunk[i] * 8;
-        if (k < p.K) {
-          const int tap = k / p.Cin;
-          const int ci = k - tap * p.Cin;
-          const int ky = tap / p.ksize;
-          const int kx = tap - ky * p.ksize;
-          int iy = cy_[i] + ky, ix = cx_[i] + kx;
-          if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) {
-            if (p.upsample) { iy >>= 1; ix >>= 1; }
-            src = A + (((long long)cbh_[i] + iy) * p.IW + ix) * p.Cin + ci;
-          }
-        }
-      } else if constexpr (CONV == 2) {            // Cin % 64, no upsample: linear tap offset
-        const int iy = cy_[i] + t_ky, ix = cx_[i] + t_kx;
-        const long long toff = ((long long)t_ky * p.IW + t_kx) * p.Cin + t_ci;   // uniform
-        if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) src = A + a_off[i] + toff;
-      } else {                                     // CONV == 3: Cin % 64 with fused 2x upsample
-        int iy = cy_[i] + t_ky, ix = cx_[i] + t_kx;
-        if ((unsigned)iy < (unsigned)Hv && (unsigned)ix < (unsigned)Wv) {
-          iy >>= 1; ix >>= 1;
-          src = A + (((long long)cbh_[i] + iy) * p.IW + ix) * p.Cin + t_ci + a_chunk[i] * 8;
-        }
-      }
-      glds16(src, As + (32 * i + 8 * wave) * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < WR; ++i) {
-      if (32 * i + 8 * wave < BN) {          // wave-uniform
-        const void* src = (w_row[i] >= 0 && (kin || k0 + w_chunk[i] * 8 < p.K)) ? (const void*)(W + w_off[i] + k0) : zp;
-        glds16(src, Ws + (32 * i + 8 * wave) * 8);
-      }
-    }
-    if constexpr (CONV >= 2) tap_next();
-  };
-
-  f32x4_t acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15;      // fragment row within 16
-  const int fq = lane >> 4;      // k-chunk within a 32-k step
-  // fragment read addresses are loop-invariant: rows 16*i + r0 share the swizzle of r0
-  // ((r0 + 16 i) >> 1) & 7 == (r0 >> 1) & 7), so each k-step needs ONE lane offset per operand
-  // and the per-fragment / per-buffer parts are ds_read immediates
-  const int w_r0 = wn * (BN / WN) + fr, a_r0 = wm * (BM / WM) + fr;
-  int w_rd[2], a_rd[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    w_rd[ks] = BM * 8 + w_r0 * 8 + swz(w_r0, ks * 4 + fq);
-    a_rd[ks] = a_r0 * 8 + swz(a_r0, ks * 4 + fq);
-  }
-  auto compute = [&](int buf) {
-    const uint4* Bs = smem + buf * TILE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t wf[TI], af[TJ];
-#pragma unroll
-      for (int i = 0; i < TI; ++i) wf[i] = as_bf16x8(Bs[w_rd[ks] + 16 * 8 * i]);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) af[j] = as_bf16x8(Bs[a_rd[ks] + 16 * 8 * j]);
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // ---- k range of this split
-  const int nk_all = (p.K + BK - 1) / BK;
-  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
-  const int kt0 = blockIdx.y * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-  if constexpr (CONV >= 2) tap_init(kt0);
-
-  if constexpr (STAGES == 2) {
-    if (nk > 0) stage(kt0, 0);
-    __syncthreads();                       // drains the DMA (vmcnt(0)) and publishes the tile
-    // unrolled by two so the LDS buffer of every stage/compute is a compile-time offset
-    for (int t = 0; t < nk; t += 2) {
-      if (t + 1 < nk) stage(kt0 + t + 1, 1);
-      compute(0);
-      __syncthreads();                     // next tile landed and everyone is done with this one
-      if (t + 1 >= nk) break;
-      if (t + 2 < nk) stage(kt0 + t + 2, 0);
-      compute(1);
-      __syncthreads();
-    }
-  } else {
-    if (nk > 0) stage(kt0, 0);
-    if (nk > 1) stage(kt0 + 1, 1);
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) wait_vmcnt<NPT>();   // retire tile t, leave tile t+1 in flight
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();        // every wave's share of tile t landed; tile t-1 is free
-      if (t + 2 < nk) stage(kt0 + t + 2, (t + 2) % 3);
-      compute(t % 3);
-    }
-  }
-
-  // ---- LDS-staged epilogue (bf16 output, no split): the MFMA layout gives each lane 4
-  // consecutive columns of one row (8-byte stores, 32 B per row per instruction); instead the
-  // tile is written to LDS (bias / time-bias / activation applied in registers) and streamed out
-  // as full rows of 16-byte stores, residual added in the same coalesced pass.
-  if constexpr (!OUTF32) {
-    constexpr int OBN = GEGLU ? BN / 2 : BN;   // output columns of this tile
-    constexpr int OST = OBN + 8;               // LDS row stride (elements): 16-B pad
-    const long long cbs = p.ldcb ? p.ldcb : p.N;
-    const bool lds_ok = gridDim.y == 1 && (p.N % 8 == 0) && (p.ldc % 8 == 0) && (cbs % 4 == 0);
-    if (lds_ok) {
-      __syncthreads();                        // every wave is done with the staging buffers
-      uint16_t* T = reinterpret_cast<uint16_t*>(smem);
-      const int hw = p.Ho * p.Wo;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int ml = wm * (BM / WM) + 16 * j + fr;
-        const int m = m0 + ml;
-        const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
-        if constexpr (GEGLU) {
-#pragma unroll
-          for (int pi = 0; pi < TI / 2; ++pi) {
-            const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;
-            const int n = n0 + nl;
-            float o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
-              if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-              o[r] = gate_f(h, g, p.act);
-            }
-            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < TI; ++i) {
-            const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
-            const int n = n0 + nl;
-            float o[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
-                          acc[i][j][3] * p.alpha};
-            if (n < p.N && m < p.M) {
-              if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
-              if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
-              if (p.act != ACT_NONE) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
-              }
-            }
-            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          }
-        }
-      }
-      __syncthreads();
-      constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
-      uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
-      for (int c = tid; c < BM * CPR; c += THREADS) {
-        const int row = c / CPR, c8 = c - row * CPR;
-        const int m = m0 + row, n = n0 + c8 * 8;
-        if (m >= p.M || n >= p.N) continue;
-        uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
-        if (p.residual) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + (long long)m * p.ldc + n);
-          float a[8], b[8];
-          unpack8(v, a);
-          unpack8(rv, b);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[e] += b[e];
-          v = pack8(a);
-        }
-        *reinterpret_cast<uint4*>(Cb + (long long)m * p.ldc + n) = v;
-      }
-      return;
-    }
-  }
-
-  // ---- direct epilogue (fp32 outputs, split-K partial slabs, ragged N)
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int m = m0 + wm * (BM / WM) + 16 * j + fr;
-    if (m >= p.M) continue;
-    if constexpr (GEGLU) {
-#pragma unroll
-      for (int pi = 0; pi < TI / 2; ++pi) {
-        const int n = n0 + wn * (BN / WN / 2) + 16 * pi + 4 * fq;
-        if (n >= p.N) continue;
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
-          if (p.bias) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-          o[r] = gate_f(h, g, p.act);
-        }
-        uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-        if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
-        *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
-        if (n >= p.N) continue;
-        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (gridDim.y > 1) {               // split-K: raw fp32 partial slab
-          float* dst = partial + ((long long)blockIdx.y * p.M + m) * p.N + n;
-          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
-          epilogue4<OUTF32>(p, batch, m, n, o);
-        }
-      }
-    }
-  }
-}
-
-template <bool OUTF32>
-__global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ partial, int split) {
-  const long long nq = (long long)p.M * (p.N / 4);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long long)gridDim.x * blockDim.x) {
-    const int m = (int)(i / (p.N / 4));
-    const int n = (int)(i - (long long)m * (p.N / 4)) * 4;
-    float o[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < split; ++s) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + ((long long)s * p.M + m) * p.N + n);
-      o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
-    }
-    epilogue4<OUTF32>(p, 0, m, n, o);
-  }
+  if (!force || p.K % BK != 0) return false;
+  const long long ldw = p.ldw ? p.ldw : p.K;
+  const long long lim = (1LL << 31) - 1;
+  if (((long long)(p.Nw - 1) * ldw + p.K) * 2 > lim) return false;
+  if (!p.conv) return ((long long)(p.M - 1) * p.lda + p.K) * 2 <= lim;
+  if (p.upsample || p.Cin % 64 != 0) return false;
+  const long long bias = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
+  return (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2 + bias <= lim;
 }
 
 // SIMT fallback for shapes the MFMA path does not take (K % 8 != 0 linear layers: the
@@ -553,114 +87,40 @@ __global__ void gemm_simt_kernel(GemmArgs p) {
     reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n] = f2bf(o);
 }
 
-int g_stages_override = -1;   // CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark)
-
-int stages_pref() {
-  if (g_stages_override < 0) {
-    const char* e = getenv("CASSMANTLE_GEMM_STAGES");
-    g_stages_override = e ? atoi(e) : 0;
-  }
-  return g_stages_override;
-}
-
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
-void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
-  const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
-  const int nM = (p.M + BM - 1) / BM;
-  const int split = (ws != nullptr && p.split > 1) ? p.split : 1;
-  dim3 grid(nN * nM, split, p.batch);
-  constexpr size_t lds = (size_t)STAGES * (BM + BN) * BK * 2;
-  // (the kernel is named once, outside any lambda: a kernel template referenced only from a
-  // lambda inside this function template was left uninstantiated by hipcc)
-  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF>;
-  if constexpr (lds > 65536) {
-    // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
-    static bool once = false;
-    if (!once) {
-      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      once = true;
-    }
-  }
-  hipLaunchKernelGGL(kfn, grid, dim3(THREADS), lds, s, p, ws);
-  if (split > 1) {
-    const long long nq = (long long)p.M * (p.N / 4);
-    const long long nb = (nq + 255) / 256;
-    const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel<OUTF32>, dim3(rb), dim3(256), 0, s, p, ws, split);
-  }
-}
-
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, bool BUF>
-void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
-  // STAGES=3 (counted vmcnt, one block/CU) measured 1.3-1.7x SLOWER than 2 stages at 2
-  // blocks/CU on every SD shape (profiles/r1_ops_stages_ab.txt); define CASSMANTLE_GEMM_3STAGE
-  // to compile it for experiments.
-#ifdef CASSMANTLE_GEMM_3STAGE
-  if constexpr (BN % 32 == 0 && !BUF) {
-    if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3, false>(p, ws, s);
-  }
-#endif
-  launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2, BUF>(p, ws, s);
-}
-
-// Tile menu (all 4 waves, 2 blocks per CU by LDS):
-//   0: 128x128 (2x2)   1: 128x160 (2x2, wave 80x64)   2: 256x64 (4x1)   3: 128x64 (2x2)   4: 256x16 (4x1)
-struct TileCfg { int BM, BN; float eff; };
-constexpr TileCfg kTiles[5] = {{128, 128, 1.00f}, {128, 160, 1.02f}, {256, 64, 0.95f}, {128, 64, 0.80f},
-                               {256, 16, 0.25f}};
-constexpr int kSlots = 512;   // resident blocks: 256 CUs x 2
-
-template <int CONV, bool OUTF32, bool BUF>
-void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
-  switch (p.cfg) {
-    case 1: launch_st<128, 160, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
-    case 2: launch_st<256, 64, 4, 1, CONV, false, OUTF32, BUF>(p, ws, s); break;
-    case 3: launch_st<128, 64, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
-    case 4: launch_st<256, 16, 4, 1, CONV, false, OUTF32, BUF>(p, ws, s); break;
-    default: launch_st<128, 128, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
-  }
-}
-
-template <int CONV, bool BUF>
-void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
-  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);
-  else if (p.out_f32) launch_cfg<CONV, true, BUF>(p, ws, s);
-  else launch_cfg<CONV, false, BUF>(p, ws, s);
-}
-
-// buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
-// 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
-bool buf_ok(const GemmArgs& p) {
-  static int force = -1;
-  if (force < 0) {
-    const char* e = getenv("CASSMANTLE_GEMM_BUF");
-    force = e ? atoi(e) : 1;
-  }
-  if (!force || p.K % BK != 0) return false;
-  const long long ldw = p.ldw ? p.ldw : p.K;
-  const long long lim = (1LL << 31) - 1;
-  if (((long long)(p.Nw - 1) * ldw + p.K) * 2 > lim) return false;
-  if (!p.conv) return ((long long)(p.M - 1) * p.lda + p.K) * 2 <= lim;
-  if (p.upsample || p.Cin % 64 != 0) return false;
-  const long long bias = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
-  return (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2 + bias <= lim;
-}
-
 }  // namespace
 
 // Choose tile config + split-K by an occupancy-round cost model: the kernel is latency-bound
 // per k-tile, so time ~ rounds(blocks / 512) x k-tiles-per-block x tile-cost; split-K adds a
 // reduction pass over split x M x N fp32.  Wave quantisation (e.g. 640 blocks = 1.25 rounds)
 // was the single largest loss on the SD shapes (M = 32768 / 8192 / 2048 / 512).
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 GemmPlan gemm_plan(const GemmArgs& p) {
   GemmPlan best{0, 1};
-  if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) return best;
+  // A/B knobs for the microbenchmark: CASSMANTLE_GEMM_CFG=<tile index>, CASSMANTLE_GEMM_SPLIT=<k slices>
+  static const int force_cfg = env_int("CASSMANTLE_GEMM_CFG", -1);
+  static const int force_split = env_int("CASSMANTLE_GEMM_SPLIT", 0);
+  static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
+  const bool gated = p.act == ACT_GEGLU || p.act == ACT_SWIGLU;
+  int only = -1;                         // forced tile (cost model still picks the split)
+  if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16))) {
+    if (gated) {
+      if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
+      return best;
+    }
+    only = force_cfg;
+  }
+  if (gated) return best;
   const int nk = (p.K + BK - 1) / BK;
   // M <= 8 goes to the GEMV path; short prompts (M = tens of rows) need split-K to fill the chip
   const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M > 8;
   double best_t = 1e30;
-  for (int c = 0; c < 5; ++c) {
+  for (int c = 0; c < kNumTiles; ++c) {
     const TileCfg& tc = kTiles[c];
+    if (only >= 0 ? c != only : (c >= 5 && !use_big)) continue;
     if (c == 4 && p.N > 16) continue;
     if (c != 4 && p.N <= 16) continue;
     const long long tiles = (long long)((p.N + tc.BN - 1) / tc.BN) * ((p.M + tc.BM - 1) / tc.BM) * p.batch;
@@ -668,7 +128,7 @@ GemmPlan gemm_plan(const GemmArgs& p) {
     for (int split = 1; split <= GEMM_MAX_SPLIT; ++split) {
       if (split > 1 && (!can_split || nk / split < 4)) break;
       const long long blocks = tiles * split;
-      const long long rounds = (blocks + kSlots - 1) / kSlots;
+      const long long rounds = (blocks + tc.slots - 1) / tc.slots;
       const int kper = (nk + split - 1) / split;
       // per-k-tile cost: fixed latency part + size part (normalised to a 128x128 tile)
       const double tile_cost = (0.55 + 0.45 * (tc.BM * tc.BN) / 16384.0) / tc.eff;
@@ -676,6 +136,7 @@ GemmPlan gemm_plan(const GemmArgs& p) {
       double t = 1.8 * rounds * (kper + 2) * tile_cost * (waste > 1.3 ? waste : 1.0);
       // split-K: slab write + read at ~3 TB/s plus the extra reduce launch (~6 us in a graph)
       if (split > 1) t += 6.0 + 2.0 * (double)split * p.M * p.N * 4 / 3.0e6;
+      if (only >= 0 && force_split > 0 && split != force_split) continue;
       if (t < best_t - 1e-9) { best_t = t; best = GemmPlan{c, split}; }
     }
   }
@@ -701,13 +162,13 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
   }
   const bool buf = buf_ok(p);
   if (!p.conv) {
-    if (buf) launch_tiles<0, true>(p, ws, s);
-    else launch_tiles<0, false>(p, ws, s);
+    if (buf) gemm_c0_buf_launch(p, ws, s);
+    else gemm_c0_launch(p, ws, s);
   } else if (p.Cin % 64 == 0) {
-    if (p.upsample) launch_tiles<3, false>(p, ws, s);
-    else if (buf) launch_tiles<2, true>(p, ws, s);
-    else launch_tiles<2, false>(p, ws, s);
+    if (p.upsample) gemm_c3_launch(p, ws, s);
+    else if (buf) gemm_c2_buf_launch(p, ws, s);
+    else gemm_c2_launch(p, ws, s);
   } else {
-    launch_tiles<1, false>(p, ws, s);
+    gemm_c1_launch(p, ws, s);
   }
 }

@@ -1,183 +1,259 @@
 // GroupNorm(+SiLU) for NHWC activations and LayerNorm.
 //
 // GroupNorm over NHWC: a group is Cg = C/G consecutive channels of every pixel, so the
-// statistics are a strided reduction.  Three small kernels, all 16-byte vectorised:
-//   1. partial sums: grid (B, chunks); each thread owns ONE 8-channel vector position of the
-//      row (blockDim = multiple of C/8) and walks rows -> per-channel sum / sum-of-squares in
-//      registers, reduced across the block's row-lanes in LDS; per-(b, chunk, channel) partials
-//      go to a small fp32 workspace.  Chunks are sized so B*chunks fills all 256 CUs even for
-//      the 512x512 VAE levels.
-//   2. finalize: per (b, group) combine partials in fp64 -> per-(b, channel) scale/shift
-//      (gamma*rstd, beta - mean*gamma*rstd).
-//   3. apply: y = x*scale + shift (+ SiLU) streamed at HBM rate.
-// LayerNorm: one wave per row, the row held in registers (two-pass mean/variance).
+// statistics are a strided reduction.  Three kernels, all 16-byte vectorised:
+//   1. stats: grid (chunks, B), 256 threads = R row-lanes x T vector-lanes (T*VPT 8-channel
+//      vectors cover a row); each thread keeps 4 rows of loads in flight and accumulates
+//      per-channel sum / sum-of-squares in registers; the block reduces row-lanes and then the
+//      Cg channels of each group in LDS and writes ONE (sum, sumsq) pair per (b, chunk, group).
+//      Chunks are sized so B*chunks ~ 512 blocks: every CU streams (the per-channel, per-chunk
+//      partials of v0 made the finalize pass read chunks*C floats per group, 5.7 us a call).
+//   2. finalize: one wave per (b, group): lane-strided chunk partials, fp64 shuffle reduce ->
+//      (mean, rstd).
+//   3. apply: grid (row-blocks, B); each thread derives the scale/shift of its channels once
+//      (gamma*rstd, beta - mean*gamma*rstd) and streams rows with no per-element index math
+//      (v0 decoded row/batch with 64-bit divisions per vector: 2.9 TB/s).
+// LayerNorm: T = 2..64 lanes per row (T*8*VPL >= D), 64/T rows per wave, row held in
+// registers, two-pass mean/variance, xor-shuffle reductions inside the T-lane segment
+// (v0 used one wave per row: 40 of 64 lanes busy at D = 320).
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
 constexpr int GN_THREADS = 256;
+constexpr int GN_UNROLL = 4;
+
+struct GnGeom { int V, VPT, T, R; };
+GnGeom gn_geom(int C) {
+  GnGeom g;
+  g.V = C / 8;
+  g.VPT = (g.V + GN_THREADS - 1) / GN_THREADS;
+  g.T = (g.V + g.VPT - 1) / g.VPT;
+  g.R = GN_THREADS / g.T;
+  if (g.R < 1) g.R = 1;
+  return g;
+}
 
 template <int VPT>
-__global__ void gn_partial_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
-                                  long long S, int C, int chunks, long long rows_per_chunk) {
-  extern __shared__ float sh[];              // [16][GN_THREADS] (row-lane reduction)
-  const int V = C / 8;                       // 8-channel vectors per row
+__global__ void __launch_bounds__(GN_THREADS) gn_stats_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                              long long S, int C, int G, int T, int R, int chunks,
+                                                              long long rows_per_chunk) {
+  extern __shared__ float sh[];              // [2][R][C] row-lane partials, then [2][C] channel sums
+  const int V = C / 8;
   const int tid = threadIdx.x;
   const int b = blockIdx.y, ck = blockIdx.x;
   const long long rbeg = (long long)ck * rows_per_chunk;
   const long long rend = min(S, rbeg + rows_per_chunk);
-  const uint16_t* base = x + ((long long)b * S) * C;
-  if (VPT > 1 || V > GN_THREADS / 2) {
-    // wide rows: each thread owns whole vector columns, no cross-thread reduction
+  const uint16_t* base = x + (long long)b * S * C;
+  const int tv = tid % T, rl = tid / T;
+  const bool active = rl < R;
+  float s[VPT][8], q[VPT][8];
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int v = tid + GN_THREADS * j;
-      if (v >= V) continue;
-      float s[8], ss[8];
+  for (int j = 0; j < VPT; ++j)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { s[i] = 0.f; ss[i] = 0.f; }
-      for (long long r = rbeg; r < rend; ++r) {
+    for (int i = 0; i < 8; ++i) { s[j][i] = 0.f; q[j][i] = 0.f; }
+  if (active) {
+    long long r = rbeg + rl;
+    for (; r + (GN_UNROLL - 1) * R < rend; r += GN_UNROLL * R) {
+      uint4 u[GN_UNROLL][VPT];
+#pragma unroll
+      for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+          const int v = tv + T * j;
+          u[k][j] = v < V ? *reinterpret_cast<const uint4*>(base + (r + (long long)k * R) * C + v * 8) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+      for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+          float f[8];
+          unpack8(u[k][j], f);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { s[j][i] += f[i]; q[j][i] = fmaf(f[i], f[i], q[j][i]); }
+        }
+    }
+    for (; r < rend; r += R) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = tv + T * j;
+        if (v >= V) continue;
         float f[8];
         unpack8(*reinterpret_cast<const uint4*>(base + r * C + v * 8), f);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { s[i] += f[i]; ss[i] = fmaf(f[i], f[i], ss[i]); }
+        for (int i = 0; i < 8; ++i) { s[j][i] += f[i]; q[j][i] = fmaf(f[i], f[i], q[j][i]); }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = tv + T * j;
+      if (v >= V) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        part[(((long long)b * chunks + ck) * 2 + 0) * C + v * 8 + i] = s[i];
-        part[(((long long)b * chunks + ck) * 2 + 1) * C + v * 8 + i] = ss[i];
+        sh[(long long)rl * C + v * 8 + i] = s[j][i];
+        sh[(long long)(R + rl) * C + v * 8 + i] = q[j][i];
       }
     }
-    return;
-  }
-  const int R = GN_THREADS / V;              // row lanes sharing a vector column
-  const bool active = tid < R * V;
-  const int v = tid % V, r0 = tid / V;
-  float s[8], ss[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { s[i] = 0.f; ss[i] = 0.f; }
-  if (active) {
-    for (long long r = rbeg + r0; r < rend; r += R) {
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(base + r * C + v * 8), f);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { s[i] += f[i]; ss[i] = fmaf(f[i], f[i], ss[i]); }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    sh[i * GN_THREADS + tid] = active ? s[i] : 0.f;
-    sh[(8 + i) * GN_THREADS + tid] = active ? ss[i] : 0.f;
   }
   __syncthreads();
-  for (int job = tid; job < V * 16; job += GN_THREADS) {
-    const int vv = job % V, comp = job / V;  // comp = stat*8 + i
+  float* cs = sh + 2LL * R * C;              // [2][C]
+  for (int c = tid; c < 2 * C; c += GN_THREADS) {
+    const int stat = c / C, ch = c - stat * C;
     float acc = 0.f;
-    for (int rr = 0; rr < R; ++rr) acc += sh[comp * GN_THREADS + rr * V + vv];
-    const int stat = comp / 8, i = comp % 8;
-    part[(((long long)b * chunks + ck) * 2 + stat) * C + vv * 8 + i] = acc;
+    for (int k = 0; k < R; ++k) acc += sh[(long long)(stat * R + k) * C + ch];
+    cs[c] = acc;
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  for (int j = tid; j < 2 * G; j += GN_THREADS) {
+    const int stat = j / G, g = j - stat * G;
+    float acc = 0.f;
+    for (int c = 0; c < Cg; ++c) acc += cs[stat * C + g * Cg + c];
+    part[(((long long)b * chunks + ck) * G + g) * 2 + stat] = acc;
   }
 }
 
-// one 64-thread block per (b, group): the chunks x Cg partials are summed in fp64 across lanes
-__global__ void gn_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ gamma,
-                                   const uint16_t* __restrict__ beta, float* __restrict__ scale,
-                                   float* __restrict__ shift, long long S, int C, int G, int chunks, float eps) {
+// one wave per (b, group): chunk partials summed in fp64 -> (mean, rstd)
+__global__ void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stats, long long S, int C,
+                                   int G, int chunks, float eps) {
   const int g = blockIdx.x, b = blockIdx.y;
-  const int Cg = C / G;
   const int lane = threadIdx.x;
   double sum = 0.0, sq = 0.0;
-  for (int j = lane; j < chunks * Cg; j += 64) {
-    const int ck = j / Cg, c = j - ck * Cg;
-    const int ch = g * Cg + c;
-    sum += part[(((long long)b * chunks + ck) * 2 + 0) * C + ch];
-    sq += part[(((long long)b * chunks + ck) * 2 + 1) * C + ch];
+  for (int ck = lane; ck < chunks; ck += 64) {
+    const float2 v = *reinterpret_cast<const float2*>(part + (((long long)b * chunks + ck) * G + g) * 2);
+    sum += v.x;
+    sq += v.y;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     sum += __shfl_xor(sum, o, 64);
     sq += __shfl_xor(sq, o, 64);
   }
-  const double n = (double)S * Cg;
-  const double mean = sum / n;
-  double var = sq / n - mean * mean;
-  if (var < 0) var = 0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  for (int c = lane; c < Cg; c += 64) {
-    const int ch = g * Cg + c;
-    const float ga = bf2f(gamma[ch]), be = bf2f(beta[ch]);
-    scale[b * C + ch] = ga * rstd;
-    shift[b * C + ch] = be - (float)mean * ga * rstd;
+  if (lane == 0) {
+    const double n = (double)S * (C / G);
+    const double mean = sum / n;
+    double var = sq / n - mean * mean;
+    if (var < 0) var = 0;
+    stats[((long long)b * G + g) * 2 + 0] = (float)mean;
+    stats[((long long)b * G + g) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
   }
 }
 
-__global__ void gn_apply_kernel(const uint16_t* __restrict__ x, const float* __restrict__ scale,
-                                const float* __restrict__ shift, uint16_t* __restrict__ y,
-                                long long S, int C, int B, int silu) {
-  const long long nvec = (long long)B * S * C / 8;
+template <int VPT>
+__global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __restrict__ x,
+                                                              const float* __restrict__ stats,
+                                                              const uint16_t* __restrict__ gamma,
+                                                              const uint16_t* __restrict__ beta,
+                                                              uint16_t* __restrict__ y, long long S, int C, int G,
+                                                              int T, int R, long long rows_per_block, int silu) {
   const int V = C / 8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
-    long long row = i / V;
-    int v = (int)(i - row * V);
-    int b = (int)(row / S);
-    uint4 u = reinterpret_cast<const uint4*>(x)[i];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int tv = tid % T, rl = tid / T;
+  if (rl >= R) return;
+  const int Cg = C / G;
+  float sc[VPT][8], sf[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int v = tv + T * j;
+    if (v >= V) continue;
+    float ga[8], be[8];
+    unpack8(*reinterpret_cast<const uint4*>(gamma + v * 8), ga);
+    unpack8(*reinterpret_cast<const uint4*>(beta + v * 8), be);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int g = (v * 8 + i) / Cg;
+      const float2 ms = *reinterpret_cast<const float2*>(stats + ((long long)b * G + g) * 2);
+      sc[j][i] = ga[i] * ms.y;
+      sf[j][i] = be[i] - ms.x * sc[j][i];
+    }
+  }
+  const long long rbeg = (long long)blockIdx.x * rows_per_block;
+  const long long rend = min(S, rbeg + rows_per_block);
+  const long long off = (long long)b * S * C;
+  const uint16_t* xb = x + off;
+  uint16_t* yb = y + off;
+  auto emit = [&](long long r, int j, uint4 u) {
     float f[8];
     unpack8(u, f);
-    const float4* sc = reinterpret_cast<const float4*>(scale + (long long)b * C + v * 8);
-    const float4* sh = reinterpret_cast<const float4*>(shift + (long long)b * C + v * 8);
-    float4 s0 = sc[0], s1 = sc[1], h0 = sh[0], h1 = sh[1];
-    float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float o = fmaf(f[k], sv[k], hv[k]);
-      f[k] = silu ? silu_f(o) : o;
+    for (int i = 0; i < 8; ++i) {
+      const float o = fmaf(f[i], sc[j][i], sf[j][i]);
+      f[i] = silu ? silu_f(o) : o;
     }
-    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+    *reinterpret_cast<uint4*>(yb + r * C + (tv + T * j) * 8) = pack8(f);
+  };
+  long long r = rbeg + rl;
+  for (; r + (GN_UNROLL - 1) * R < rend; r += GN_UNROLL * R) {
+    uint4 u[GN_UNROLL][VPT];
+#pragma unroll
+    for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = tv + T * j;
+        if (v < V) u[k][j] = *reinterpret_cast<const uint4*>(xb + (r + (long long)k * R) * C + v * 8);
+      }
+#pragma unroll
+    for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+        if (tv + T * j < V) emit(r + (long long)k * R, j, u[k][j]);
   }
+  for (; r < rend; r += R)
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+      if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(xb + r * C + (tv + T * j) * 8));
 }
 
-// LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): one wave per row; D <= 64*8*MAXV
-template <int MAXV, bool RMS>
+// LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): T lanes per row, VPL vectors per lane
+template <int VPL, bool RMS>
 __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gamma,
                           const uint16_t* __restrict__ beta, uint16_t* __restrict__ y,
-                          long long rows, int D, float eps) {
+                          long long rows, int D, int T, float eps) {
   const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int seg = lane / T, sl = lane - seg * T;
+  const int rows_per_wave = 64 / T;
+  const long long row = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * rows_per_wave + seg;
+  const bool ok = row < rows;
   const int V = D / 8;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + row * D);
-  float f[MAXV][8];
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (ok ? row : 0) * D);
+  float f[VPL][8];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int v = lane + 64 * j;
-    if (v < V) {
+  for (int j = 0; j < VPL; ++j) {
+    const int v = sl + T * j;
+    if (ok && v < V) {
       unpack8(xr[v], f[j]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += f[j][k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[j][k] = 0.f;
     }
   }
-  const float mean = RMS ? 0.f : wave_sum(s) / D;
+  // segment reductions: xor offsets < T stay inside the T-lane segment
+  for (int o = T >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = RMS ? 0.f : s / D;
   float ss = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int v = lane + 64 * j;
+  for (int j = 0; j < VPL; ++j) {
+    const int v = sl + T * j;
     if (v < V) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { float t = f[j][k] - mean; ss = fmaf(t, t, ss); }
+      for (int k = 0; k < 8; ++k) { const float t = f[j][k] - mean; ss = fmaf(t, t, ss); }
     }
   }
-  const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+  for (int o = T >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float rstd = rsqrtf(ss / D + eps);
+  if (!ok) return;
   uint4* yr = reinterpret_cast<uint4*>(y + row * D);
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int v = lane + 64 * j;
+  for (int j = 0; j < VPL; ++j) {
+    const int v = sl + T * j;
     if (v < V) {
-      uint4 gu = reinterpret_cast<const uint4*>(gamma)[v];
       float g[8], bb[8];
-      unpack8(gu, g);
+      unpack8(reinterpret_cast<const uint4*>(gamma)[v], g);
       if (beta) unpack8(reinterpret_cast<const uint4*>(beta)[v], bb);
       else for (int k = 0; k < 8; ++k) bb[k] = 0.f;
       float o[8];
@@ -188,9 +264,9 @@ __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __rest
   }
 }
 
-int gn_chunks(int B, long long S) {
-  long long want = (1024 + B - 1) / B;             // ~4 blocks per CU in total
-  long long maxc = (S + 63) / 64;                  // at least 64 rows per chunk
+int gn_chunks(int B, long long S, int R) {
+  long long want = (512 + B - 1) / B;                      // ~2 blocks per CU in total
+  long long maxc = (S + 4LL * R - 1) / (4LL * R);          // >= one unrolled row group per lane
   long long ch = want < maxc ? want : maxc;
   return (int)(ch < 1 ? 1 : ch);
 }
@@ -198,40 +274,66 @@ int gn_chunks(int B, long long S) {
 }  // namespace
 
 long long group_norm_workspace(int B, long long S, int C) {
-  int chunks = gn_chunks(B, S);
-  return (long long)B * chunks * 2 * C + 2LL * B * C;   // floats
+  const GnGeom g = gn_geom(C);
+  const int chunks = gn_chunks(B, S, g.R);
+  return (long long)B * chunks * 2 * C + 2LL * B * C;   // floats (>= partials + stats for any G)
 }
 
 void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        float* ws, int B, long long S, int C, int G, float eps, int silu, hipStream_t s) {
-  const int chunks = gn_chunks(B, S);
+  const GnGeom g = gn_geom(C);
+  const int chunks = gn_chunks(B, S, g.R);
   const long long rpc = (S + chunks - 1) / chunks;
   float* part = ws;
-  float* scale = ws + (long long)B * chunks * 2 * C;
-  float* shift = scale + (long long)B * C;
-  const int V = C / 8;
-  dim3 g1(chunks, B);
-  size_t sh = sizeof(float) * 16 * GN_THREADS;
-  if (V <= GN_THREADS)
-    hipLaunchKernelGGL(gn_partial_kernel<1>, g1, dim3(GN_THREADS), sh, s, x, part, S, C, chunks, rpc);
+  float* stats = ws + (long long)B * chunks * G * 2;
+  const size_t shs = sizeof(float) * (2LL * g.R * C + 2LL * C);
+  if (g.VPT == 1)
+    hipLaunchKernelGGL(gn_stats_kernel<1>, dim3(chunks, B), dim3(GN_THREADS), shs, s, x, part, S, C, G, g.T, g.R,
+                       chunks, rpc);
   else
-    hipLaunchKernelGGL(gn_partial_kernel<2>, g1, dim3(GN_THREADS), sh, s, x, part, S, C, chunks, rpc);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(G, B), dim3(64), 0, s, part, gamma, beta, scale, shift, S, C, G, chunks, eps);
-  long long nvec = (long long)B * S * C / 8;
-  long long blocks = (nvec + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, scale, shift, y, S, C, B, silu);
+    hipLaunchKernelGGL(gn_stats_kernel<2>, dim3(chunks, B), dim3(GN_THREADS), shs, s, x, part, S, C, G, g.T, g.R,
+                       chunks, rpc);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(G, B), dim3(64), 0, s, part, stats, S, C, G, chunks, eps);
+  // apply: ~8 rows per row-lane per block
+  long long rpb = 8LL * g.R;
+  long long nb = (S + rpb - 1) / rpb;
+  if (nb * B < 1024) {                                     // small images: shorter blocks, more of them
+    rpb = (long long)g.R * 2;
+    nb = (S + rpb - 1) / rpb;
+  }
+  if (g.VPT == 1)
+    hipLaunchKernelGGL(gn_apply_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), 0, s, x, stats, gamma, beta, y, S,
+                       C, G, g.T, g.R, rpb, silu);
+  else
+    hipLaunchKernelGGL(gn_apply_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), 0, s, x, stats, gamma, beta, y, S,
+                       C, G, g.T, g.R, rpb, silu);
+}
+
+template <int VPL, bool RMS>
+static void launch_ln_t(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                        long long rows, int D, int T, float eps, hipStream_t s) {
+  const long long rows_per_block = 4LL * (64 / T);
+  dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block));
+  hipLaunchKernelGGL((ln_kernel<VPL, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, T, eps);
 }
 
 template <bool RMS>
 static void launch_ln(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                       long long rows, int D, float eps, hipStream_t s) {
   const int V = D / 8;
-  dim3 grid((unsigned)((rows + 3) / 4));
-  if (V <= 64) hipLaunchKernelGGL((ln_kernel<1, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else if (V <= 128) hipLaunchKernelGGL((ln_kernel<2, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else if (V <= 256) hipLaunchKernelGGL((ln_kernel<4, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
-  else hipLaunchKernelGGL((ln_kernel<8, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, eps);
+  int T = 1;
+  while (T < 64 && T * 8 < V) T <<= 1;                 // VPL <= 8 (D <= 4096)
+  const int VPL = (V + T - 1) / T;
+  switch (VPL) {
+    case 1: launch_ln_t<1, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 2: launch_ln_t<2, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 3: launch_ln_t<3, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 4: launch_ln_t<4, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 5: launch_ln_t<5, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 6: launch_ln_t<6, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 7: launch_ln_t<7, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    default: launch_ln_t<8, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+  }
 }
 
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,

@@ -106,6 +106,9 @@ def test_conv_epilogue_fusions():
     ((2, 8, 8, 2560), 32, True, 1e-5),
     ((3, 5, 7, 64), 8, True, 1e-5),
     ((2, 4096, 320), 32, False, 1e-6),
+    ((1, 128, 128, 128), 32, True, 1e-6),      # VAE-like: Cg = 4, many chunks
+    ((8, 8, 8, 1920), 32, True, 1e-5),        # up-block concat width, Cg = 60
+    ((8, 64, 64, 640), 32, True, 1e-5),       # Cg = 20 straddles the 8-channel vectors
 ])
 def test_group_norm(shape, G, silu, eps):
     x = rnd(*shape, seed=19) + 0.5
@@ -117,9 +120,10 @@ def test_group_norm(shape, G, silu, eps):
     assert rel_err(out, exp) < 1e-2
 
 
-@pytest.mark.parametrize("D", [320, 384, 768, 1280, 32])
-def test_layer_norm(D):
-    x = rnd(333, D, seed=22) * 2 + 1
+@pytest.mark.parametrize("D,rows", [(320, 333), (384, 333), (768, 333), (1280, 333), (32, 333), (640, 1),
+                                    (4096, 7), (136, 45)])
+def test_layer_norm(D, rows):
+    x = rnd(rows, D, seed=22) * 2 + 1
     g = rnd(D, seed=23) * 0.5 + 1
     b = rnd(D, seed=24) * 0.1
     assert rel_err(ops.layer_norm(x, g, b, 1e-5), ref.layer_norm(x, g, b, 1e-5)) < 1e-2

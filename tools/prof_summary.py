@@ -1,0 +1,37 @@
+"""Summarise a rocprofv3 kernel trace: time per (kernel, grid) and per kernel family.
+
+    python tools/prof_summary.py gpurun_out/prof_q/run_kernel_trace.csv [--top 40] [--per N]
+--per N divides totals by N (e.g. the number of UNet evaluations in the traced run).
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--per", type=float, default=1.0)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    by_grid = collections.defaultdict(lambda: [0, 0.0])
+    fam = collections.defaultdict(float)
+    for r in rows:
+        n = r["Kernel_Name"].replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        key = (n[:70], r["Grid_Size_X"], r["Grid_Size_Y"])
+        by_grid[key][0] += 1
+        by_grid[key][1] += d
+        fam[re.split(r"[<(]", n)[0]] += d
+    tot = sum(v[1] for v in by_grid.values())
+    print(f"total {tot / 1e3:.2f} ms  (per unit: {tot / 1e3 / a.per:.3f} ms)")
+    for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:20]:
+        print(f"  {v / 1e3 / a.per:8.3f} ms {100 * v / tot:5.1f}%  {k}")
+    for k, v in sorted(by_grid.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"{v[1] / 1e3 / a.per:8.3f}ms {100 * v[1] / tot:5.1f}% n={v[0]:5d} avg={v[1] / v[0]:8.1f}us {k}")
+
+
+if __name__ == "__main__":
+    main()
