@@ -14,6 +14,7 @@ mapped in (``models/weights.py``); weights are random-init by default (BASELINE.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -35,6 +36,58 @@ def _ones(shape, dtype) -> nn.Parameter:
     return nn.Parameter(torch.ones(*shape, dtype=dtype), requires_grad=False)
 
 
+_GN_FUSE = os.environ.get("CASSMANTLE_GN_FUSE", "1") != "0"   # A/B knob (0: two-pass GroupNorm)
+
+
+class StatsArena:
+    """GroupNorm statistics produced by GEMM/conv epilogues: one zeroed fp32 slab per forward.
+
+    A producer (conv / linear called with ``stats=arena.take(...)``) accumulates the
+    per-(image, channel) sum and sum-of-squares of its output in its epilogue; the GroupNorm
+    that consumes the tensor then runs only its apply pass (no statistics read of the
+    activation).  All slices of one forward come from ONE buffer cleared by ONE memset in
+    :meth:`begin`.  Buffers are kept per activation shape and never reallocated once sized, so
+    a captured denoise graph keeps valid addresses: the first forward of a shape only measures
+    the slab (its slices are plain ``torch.zeros``); later forwards — including the
+    graph-capture warmups — slice the slab.  Disabled (``take`` returns None) off the HIP path,
+    where GroupNorm computes its own statistics."""
+
+    def __init__(self) -> None:
+        self._bufs: dict = {}
+        self._need: dict = {}
+        self.key = None
+        self.buf: Optional[torch.Tensor] = None
+        self.off = 0
+        self.on = False
+
+    def begin(self, key, x: torch.Tensor) -> "StatsArena":
+        self.on = x.device.type == "cuda" and ops.get_mode() == "hip" and _GN_FUSE
+        self.key, self.off = key, 0
+        if not self.on:
+            return self
+        self.buf = self._bufs.get(key)
+        need = self._need.get(key, 0)
+        if need and self.buf is None:
+            self.buf = self._bufs[key] = torch.empty(need, device=x.device, dtype=torch.float32)
+        if self.buf is not None:
+            self.buf.zero_()
+        self.device = x.device
+        return self
+
+    def take(self, B: int, C: int) -> Optional[torch.Tensor]:
+        if not self.on:
+            return None
+        n = B * C * 2
+        end = self.off + n
+        if self.buf is not None and end <= self.buf.numel():
+            s = self.buf[self.off:end].view(B, C, 2)
+        else:
+            self._need[self.key] = max(self._need.get(self.key, 0), end)
+            s = torch.zeros((B, C, 2), device=self.device, dtype=torch.float32)
+        self.off = end
+        return s
+
+
 class Linear(nn.Module):
     def __init__(self, fin: int, fout: int, bias: bool = True, gen=None, dtype=torch.bfloat16,
                  std: Optional[float] = None):
@@ -43,8 +96,8 @@ class Linear(nn.Module):
         self.weight = _param((fout, fin), std if std is not None else 1.0 / math.sqrt(fin), gen, dtype)
         self.bias = _param((fout,), 0.02, gen, dtype) if bias else None
 
-    def forward(self, x, residual=None, act=None):
-        return ops.linear(x, self.weight, self.bias, residual=residual, act=act)
+    def forward(self, x, residual=None, act=None, stats=None):
+        return ops.linear(x, self.weight, self.bias, residual=residual, act=act, stats=stats)
 
 
 class Conv2d(nn.Module):
@@ -58,11 +111,11 @@ class Conv2d(nn.Module):
         self.weight = _param((cout, k, k, cin), 1.0 / math.sqrt(cin * k * k), gen, dtype)
         self.bias = _param((cout,), 0.02, gen, dtype) if bias else None
 
-    def forward(self, x, residual=None, upsample=False, chan_bias=None):
+    def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None):
         if self.k == 1 and self.stride == 1 and not upsample and chan_bias is None:
-            return ops.linear(x, self.weight.view(self.cout, self.cin), self.bias, residual=residual)
+            return ops.linear(x, self.weight.view(self.cout, self.cin), self.bias, residual=residual, stats=stats)
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, residual=residual,
-                          upsample=upsample, chan_bias=chan_bias)
+                          upsample=upsample, chan_bias=chan_bias, stats=stats)
 
 
 class GroupNorm(nn.Module):
@@ -72,8 +125,10 @@ class GroupNorm(nn.Module):
         self.weight = _ones((channels,), dtype)
         self.bias = _zeros((channels,), dtype)
 
-    def forward(self, x, silu=False):
-        return ops.group_norm(x, self.groups, self.weight, self.bias, self.eps, silu)
+    def forward(self, x, silu=False, stats=None, stats2=None):
+        """``stats`` / ``stats2``: producer statistics (see :class:`StatsArena`); ``stats2``
+        covers the trailing channels of a channel concatenation."""
+        return ops.group_norm(x, self.groups, self.weight, self.bias, self.eps, silu, stats=stats, stats2=stats2)
 
 
 class LayerNorm(nn.Module):

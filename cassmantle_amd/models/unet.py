@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from .. import ops
 from .layers import (Conv2d, CrossAttention, GEGLUFeedForward, GroupNorm, LayerNorm, Linear,
-                     SelfAttention)
+                     SelfAttention, StatsArena)
 
 
 @dataclass
@@ -70,16 +70,22 @@ class ResnetBlock(nn.Module):
         self.conv2 = Conv2d(cout, cout, 3, gen=gen, dtype=dtype)
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0, gen=gen, dtype=dtype) if cin != cout else None
 
-    def forward(self, x, temb_silu, tb_all=None):
-        h = self.norm1(x, silu=True)
+    def forward(self, x, temb_silu, tb_all=None, arena: Optional[StatsArena] = None, xs=None, xs2=None):
+        """``xs`` / ``xs2``: epilogue statistics of x (of its two halves for an up-block skip
+        concatenation).  Returns (out, statistics of out or None)."""
+        B = x.shape[0]
+        cout = self.conv1.cout
+        h = self.norm1(x, silu=True, stats=xs, stats2=xs2)
         if tb_all is not None:                                   # slice of the UNet-wide batched GEMM
             tb = tb_all[:, self._tb_off:self._tb_off + self.time_emb_proj.fout]
         else:
             tb = self.time_emb_proj(temb_silu)                   # [B, cout]
-        h = self.conv1(h, chan_bias=tb)                          # time-emb add fused in epilogue
-        h = self.norm2(h, silu=True)
+        s1 = arena.take(B, cout) if arena is not None else None
+        h = self.conv1(h, chan_bias=tb, stats=s1)                # time-emb add fused in epilogue
+        h = self.norm2(h, silu=True, stats=s1)                   # statistics from conv1's epilogue
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
-        return self.conv2(h, residual=sc)                        # residual fused in epilogue
+        s2 = arena.take(B, cout) if arena is not None else None
+        return self.conv2(h, residual=sc, stats=s2), s2          # residual fused in epilogue
 
 
 class BasicTransformerBlock(nn.Module):
@@ -108,13 +114,14 @@ class Transformer2D(nn.Module):
             [BasicTransformerBlock(dim, heads, ctx_dim, gen, dtype) for _ in range(depth)])
         self.proj_out = Linear(dim, dim, gen=gen, dtype=dtype)
 
-    def forward(self, x, ctx, fp8=False):
+    def forward(self, x, ctx, fp8=False, arena: Optional[StatsArena] = None, xs=None):
         B, H, W, C = x.shape
-        h = self.norm(x).view(B, H * W, C)
+        h = self.norm(x, stats=xs).view(B, H * W, C)
         h = self.proj_in(h)
         for blk in self.transformer_blocks:
             h = blk(h, ctx, fp8=fp8)
-        return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
+        so = arena.take(B, C) if arena is not None else None
+        return self.proj_out(h, residual=x.view(B, H * W, C), stats=so).view(B, H, W, C), so
 
 
 class Downsample(nn.Module):
@@ -122,8 +129,9 @@ class Downsample(nn.Module):
         super().__init__()
         self.conv = Conv2d(c, c, 3, stride=2, padding=1, gen=gen, dtype=dtype)
 
-    def forward(self, x):
-        return self.conv(x)
+    def forward(self, x, arena: Optional[StatsArena] = None):
+        so = arena.take(x.shape[0], self.conv.cout) if arena is not None else None
+        return self.conv(x, stats=so), so
 
 
 class Upsample(nn.Module):
@@ -131,8 +139,9 @@ class Upsample(nn.Module):
         super().__init__()
         self.conv = Conv2d(c, c, 3, gen=gen, dtype=dtype)
 
-    def forward(self, x):
-        return self.conv(x, upsample=True)                       # nearest-2x fused into conv
+    def forward(self, x, arena: Optional[StatsArena] = None):
+        so = arena.take(x.shape[0], self.conv.cout) if arena is not None else None
+        return self.conv(x, upsample=True, stats=so), so         # nearest-2x fused into conv
 
 
 class UNet(nn.Module):
@@ -188,6 +197,7 @@ class UNet(nn.Module):
             self.up.append(blk)
         self.conv_norm_out = GroupNorm(g, cur, eps, dtype)
         self.conv_out = Conv2d(cur, cfg.out_channels, 3, gen=gen, dtype=dtype)
+        self._arena = StatsArena()
 
     # ------------------------------------------------------------------
     def time_embed(self, t: torch.Tensor, added: Optional[dict] = None) -> torch.Tensor:
@@ -259,29 +269,38 @@ class UNet(nn.Module):
             self.fuse_projections()
         temb = self.time_embed(t, added)
         tb = ops.linear(temb, self._tb_w, self._tb_b)               # all ResNets' time biases
-        h = self.conv_in(x)
-        skips = [h]
+        # every producer of a GroupNorm input (conv_in, ResNet conv1/conv2, transformer
+        # proj_out, down/up-sample convs) accumulates the output statistics in its epilogue,
+        # so the 61 GroupNorms of a step run their apply pass only
+        ar = self._arena.begin(tuple(x.shape), x)
+        B = x.shape[0]
+        hs = ar.take(B, self.conv_in.cout)
+        h = self.conv_in(x, stats=hs)
+        skips = [(h, hs)]
         for blk in self.down:
             for j, res in enumerate(blk.resnets):
-                h = res(h, temb, tb)
+                h, hs = res(h, temb, tb, ar, hs)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ctx, fp8)
-                skips.append(h)
+                    h, hs = blk.attentions[j](h, ctx, fp8, ar, hs)
+                skips.append((h, hs))
             if blk.downsampler is not None:
-                h = blk.downsampler(h)
-                skips.append(h)
-        h = self.mid_res1(h, temb, tb)
-        h = self.mid_attn(h, ctx, fp8)
-        h = self.mid_res2(h, temb, tb)
+                h, hs = blk.downsampler(h, ar)
+                skips.append((h, hs))
+        h, hs = self.mid_res1(h, temb, tb, ar, hs)
+        h, hs = self.mid_attn(h, ctx, fp8, ar, hs)
+        h, hs = self.mid_res2(h, temb, tb, ar, hs)
         for blk in self.up:
             for j, res in enumerate(blk.resnets):
-                h = torch.cat([h, skips.pop()], dim=-1)
-                h = res(h, temb, tb)
+                sk, sks = skips.pop()
+                h = torch.cat([h, sk], dim=-1)
+                # statistics of the concatenation = (statistics of h, statistics of the skip)
+                two = hs is not None and sks is not None
+                h, hs = res(h, temb, tb, ar, hs if two else None, sks if two else None)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ctx, fp8)
+                    h, hs = blk.attentions[j](h, ctx, fp8, ar, hs)
             if blk.upsampler is not None:
-                h = blk.upsampler(h)
-        h = self.conv_norm_out(h, silu=True)
+                h, hs = blk.upsampler(h, ar)
+        h = self.conv_norm_out(h, silu=True, stats=hs)
         return self.conv_out(h)
 
 

@@ -9,13 +9,13 @@ activations of the whole pipeline (memory-bound convs), NHWC keeps them GEMM-sha
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
 
 from .. import ops
-from .layers import Conv2d, GroupNorm, Linear
+from .layers import Conv2d, GroupNorm, Linear, StatsArena
 
 
 @dataclass
@@ -43,11 +43,15 @@ class VAEResnet(nn.Module):
         self.conv2 = Conv2d(cout, cout, 3, gen=gen, dtype=dtype)
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0, gen=gen, dtype=dtype) if cin != cout else None
 
-    def forward(self, x):
-        h = self.conv1(self.norm1(x, silu=True))
-        h = self.norm2(h, silu=True)
+    def forward(self, x, arena: Optional[StatsArena] = None, xs=None):
+        """-> (out, epilogue statistics of out or None); see :class:`StatsArena`."""
+        B = x.shape[0]
+        s1 = arena.take(B, self.conv1.cout) if arena is not None else None
+        h = self.conv1(self.norm1(x, silu=True, stats=xs), stats=s1)
+        h = self.norm2(h, silu=True, stats=s1)
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
-        return self.conv2(h, residual=sc)
+        s2 = arena.take(B, self.conv2.cout) if arena is not None else None
+        return self.conv2(h, residual=sc, stats=s2), s2
 
 
 class VAEAttention(nn.Module):
@@ -59,12 +63,14 @@ class VAEAttention(nn.Module):
         self.to_qkv = Linear(c, 3 * c, gen=gen, dtype=dtype)
         self.to_out = Linear(c, c, gen=gen, dtype=dtype)
 
-    def forward(self, x):
+    def forward(self, x, arena: Optional[StatsArena] = None, xs=None):
         B, H, W, C = x.shape
-        h = self.group_norm(x).view(B, H * W, C)
+        h = self.group_norm(x, stats=xs).view(B, H * W, C)
         qkv = self.to_qkv(h).view(B, H * W, 3, 1, C)
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
-        return self.to_out(o.reshape(B, H * W, C), residual=x.view(B, H * W, C)).view(B, H, W, C)
+        so = arena.take(B, C) if arena is not None else None
+        out = self.to_out(o.reshape(B, H * W, C), residual=x.view(B, H * W, C), stats=so)
+        return out.view(B, H, W, C), so
 
 
 class VAEDecoder(nn.Module):
@@ -91,21 +97,26 @@ class VAEDecoder(nn.Module):
             self.up.append(blk)
         self.conv_norm_out = GroupNorm(g, cur, eps, dtype)
         self.conv_out = Conv2d(cur, cfg.out_channels, 3, gen=gen, dtype=dtype)
+        self._arena = StatsArena()
 
     def forward(self, z: torch.Tensor) -> torch.Tensor:
         """z: scaled latents [B, h, w, 4] NHWC -> image [B, 8h, 8w, 3] in [-1, 1] (model dtype)."""
         z = (z.float() / self.cfg.scaling_factor).to(self.conv_in.weight.dtype)
         h = self.post_quant_conv(z)
-        h = self.conv_in(h)
-        h = self.mid_res1(h)
-        h = self.mid_attn(h)
-        h = self.mid_res2(h)
+        ar = self._arena.begin(tuple(z.shape), z)
+        B = z.shape[0]
+        hs = ar.take(B, self.conv_in.cout)
+        h = self.conv_in(h, stats=hs)
+        h, hs = self.mid_res1(h, ar, hs)
+        h, hs = self.mid_attn(h, ar, hs)
+        h, hs = self.mid_res2(h, ar, hs)
         for blk in self.up:
             for r in blk.resnets:
-                h = r(h)
+                h, hs = r(h, ar, hs)
             if blk.upsample_conv is not None:
-                h = blk.upsample_conv(h, upsample=True)
-        h = self.conv_norm_out(h, silu=True)
+                hs = ar.take(B, blk.upsample_conv.cout)
+                h = blk.upsample_conv(h, upsample=True, stats=hs)
+        h = self.conv_norm_out(h, silu=True, stats=hs)
         return self.conv_out(h)
 
     def decode_uint8(self, z: torch.Tensor) -> torch.Tensor:

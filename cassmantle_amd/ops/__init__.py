@@ -49,13 +49,38 @@ _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "
 
 
 # ----------------------------------------------------------------------------- GEMM (K6)
+def channel_stats_ref(y: torch.Tensor, stats: torch.Tensor) -> None:
+    """stats[b, c] += (sum, sum of squares) of y[b, ..., c] (the fused-epilogue contract)."""
+    B, C = y.shape[0], y.shape[-1]
+    yf = y.reshape(B, -1, C).float()
+    stats[..., 0] += yf.sum(1)
+    stats[..., 1] += (yf * yf).sum(1)
+
+
+def channel_stats(y: torch.Tensor, stats: torch.Tensor) -> None:
+    """Accumulate per-(image, channel) statistics of an NHWC / [B, N, C] tensor into ``stats``."""
+    if _use_hip(y):
+        ext().channel_stats(y.contiguous(), stats)
+    else:
+        channel_stats_ref(y, stats)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
-           residual: Optional[torch.Tensor] = None, act: Optional[str] = None) -> torch.Tensor:
-    """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu)."""
+           residual: Optional[torch.Tensor] = None, act: Optional[str] = None,
+           stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu).
+
+    ``stats`` (fp32 [B, N, 2], zeroed; B = x.shape[0]): per-(image, channel) sum and
+    sum-of-squares of y are accumulated into it by the GEMM epilogue, for a following
+    :func:`group_norm` (no statistics pass over y)."""
     if not _use_hip(x):
         if x.device.type == "cuda":  # explicit torch baseline mode: stock ops in bf16
-            return _torch_linear(x, w, bias, residual, act)
-        return ref.linear(x, w, bias, residual, act)
+            y = _torch_linear(x, w, bias, residual, act)
+        else:
+            y = ref.linear(x, w, bias, residual, act)
+        if stats is not None:
+            channel_stats_ref(y, stats)
+        return y
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
     if not x2.is_contiguous():
@@ -63,7 +88,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     N = w.shape[0] // 2 if act in ("geglu", "swiglu") else w.shape[0]
     out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
     r2 = residual.reshape(-1, N) if residual is not None else None
-    ext().gemm(x2, w, bias, r2, out, _ACT[act])
+    hw = x2.shape[0] // x.shape[0] if stats is not None else 0
+    ext().gemm(x2, w, bias, r2, out, _ACT[act], stats, hw)
     return out.reshape(*x.shape[:-1], N)
 
 
@@ -92,12 +118,17 @@ def _torch_linear(x, w, bias, residual, act):
 # ----------------------------------------------------------------------------- conv (K4/K5/K12)
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
            padding: int = 1, residual: Optional[torch.Tensor] = None, upsample: bool = False,
-           chan_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """NHWC implicit-GEMM convolution.  x [B,H,W,Cin], w [Cout,kh,kw,Cin]."""
+           chan_bias: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NHWC implicit-GEMM convolution.  x [B,H,W,Cin], w [Cout,kh,kw,Cin].  ``stats``: see
+    :func:`linear` (per-(image, Cout) output statistics for a following GroupNorm)."""
     if not _use_hip(x):
         if x.device.type == "cuda":
-            return _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias)
-        return ref.conv2d(x, w, bias, stride, padding, residual, upsample, chan_bias)
+            y = _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias)
+        else:
+            y = ref.conv2d(x, w, bias, stride, padding, residual, upsample, chan_bias)
+        if stats is not None:
+            channel_stats_ref(y, stats)
+        return y
     B, H, W, Cin = x.shape
     Cout, kh, kw, _ = w.shape
     if Cin % 8 != 0:
@@ -111,7 +142,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     Ho = (Hi + 2 * padding - kh) // stride + 1
     Wo = (Wi + 2 * padding - kw) // stride + 1
     out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=x.dtype)
-    ext().conv2d(x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample))
+    ext().conv2d(x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample), stats)
     return out
 
 
@@ -132,8 +163,37 @@ def _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias):
 
 
 # ----------------------------------------------------------------------------- norms (K7/K8)
+def _group_norm_from_stats_ref(x, num_groups, weight, bias, eps, silu, stats):
+    B, C = x.shape[0], x.shape[-1]
+    S = x.numel() // (B * C)
+    st = stats.double().view(B, num_groups, C // num_groups, 2).sum(2)     # [B, G, 2]
+    n = S * (C // num_groups)
+    mean = st[..., 0] / n
+    var = (st[..., 1] / n - mean * mean).clamp_min(0)
+    rstd = (var + eps).rsqrt()
+    cg = C // num_groups
+    mean_c = mean.repeat_interleave(cg, 1).float()                         # [B, C]
+    rstd_c = rstd.repeat_interleave(cg, 1).float()
+    shape = [B] + [1] * (x.dim() - 2) + [C]
+    y = (x.float() - mean_c.view(shape)) * rstd_c.view(shape) * weight.float() + bias.float()
+    if silu:
+        y = torch.nn.functional.silu(y)
+    return y.to(x.dtype)
+
+
 def group_norm(x: torch.Tensor, num_groups: int, weight: torch.Tensor, bias: torch.Tensor,
-               eps: float, silu: bool = False) -> torch.Tensor:
+               eps: float, silu: bool = False, stats: Optional[torch.Tensor] = None,
+               stats2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GroupNorm(+SiLU) over NHWC channels.  With ``stats`` (fp32 [B, C, 2] accumulated by the
+    producing GEMM/conv; for a channel concatenation ``stats`` covers the first channels and
+    ``stats2`` the rest) the kernel skips its statistics pass."""
+    if stats is not None:
+        if not _use_hip(x):
+            st = stats if stats2 is None else torch.cat([stats, stats2], dim=1)
+            return _group_norm_from_stats_ref(x, num_groups, weight, bias, eps, silu, st)
+        out = torch.empty_like(x)
+        ext().group_norm_stats(x.contiguous(), stats, stats2, weight, bias, out, num_groups, float(eps), int(silu))
+        return out
     if not _use_hip(x):
         if x.device.type == "cuda":
             import torch.nn.functional as F

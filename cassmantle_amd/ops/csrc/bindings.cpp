@@ -27,20 +27,43 @@ const uint16_t* opt_bptr(const c10::optional<at::Tensor>& t) {
 
 // plans split-K and allocates its fp32 partial slabs from the caching allocator (graph-pool
 // safe inside a capture), then launches on the current stream
+float* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t);
+  CHECK_CONTIG(*t);
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == images * N * 2,
+              "stats must be a zeroed fp32 [images, N, 2] tensor");
+  return t->data_ptr<float>();
+}
+
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
+  // output statistics are fused into the LDS-staged bf16 epilogue; shapes that take another
+  // path (fp32 out, GEMV rows, batched, gated, split-K reduce pass) get a separate per-channel
+  // statistics pass over the output
+  TORCH_CHECK(p.stats == nullptr || (p.N % 8 == 0 && p.ldc == p.N),
+              "gemm/conv2d stats: the output channel count must be a multiple of 8 (GroupNorm consumers)");
   const GemmPlan plan = gemm_plan(p);
   p.cfg = plan.cfg;
   p.split = plan.split;
+  float* post_stats = nullptr;
+  if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || p.batch != 1 || p.split > 1 || p.act == 4 || p.act == 6)) {
+    post_stats = p.stats;
+    p.stats = nullptr;
+  }
   if (p.split > 1) {
     auto ws = at::empty({(long long)p.split * p.M * p.N}, like.options().dtype(at::kFloat));
     launch_gemm(p, ws.data_ptr<float>(), cur_stream());
   } else {
     launch_gemm(p, nullptr, cur_stream());
   }
+  if (post_stats != nullptr)
+    launch_channel_stats(reinterpret_cast<const uint16_t*>(p.C), post_stats, p.M / p.stats_hw, p.stats_hw, p.N,
+                         cur_stream());
 }
 
 void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
-          const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act) {
+          const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act,
+          const c10::optional<at::Tensor>& stats, int64_t stats_hw) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
@@ -62,6 +85,11 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     CHECK_BF16(out);
   }
   p.C = out.data_ptr();
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats_hw > 0 && p.M % stats_hw == 0, "gemm: stats_hw must divide the rows");
+    p.stats_hw = (int)stats_hw;
+    p.stats = opt_stats(stats, p.M / stats_hw, p.N);
+  }
   run_gemm(p, out);
 }
 
@@ -88,7 +116,7 @@ void gemm_rms(const at::Tensor& x, const at::Tensor& gamma, double eps, const at
 
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
             const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& chan_bias, at::Tensor& out,
-            int64_t stride, int64_t pad, int64_t upsample) {
+            int64_t stride, int64_t pad, int64_t upsample, const c10::optional<at::Tensor>& stats) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out); CHECK_BF16(out);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "conv2d: NHWC 4-D tensors expected");
   GemmArgs p;
@@ -115,6 +143,8 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   if (chan_bias.has_value() && chan_bias->defined())
     TORCH_CHECK(chan_bias->size(0) == x.size(0) && chan_bias->size(1) == p.N, "conv2d: chan_bias must be [B, Cout]");
   p.C = out.data_ptr();
+  p.stats_hw = p.Ho * p.Wo;
+  p.stats = opt_stats(stats, x.size(0), p.N);
   run_gemm(p, out);
 }
 
@@ -149,6 +179,41 @@ void group_norm(const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& 
   auto ws = at::empty({group_norm_workspace(B, S, C)}, x.options().dtype(at::kFloat));
   launch_group_norm(bptr(x), bptr(gamma), bptr(beta), bptr_mut(out), ws.data_ptr<float>(), B, S, C, (int)groups,
                     (float)eps, (int)silu, cur_stream());
+}
+
+// GroupNorm from producer statistics: stats_a [B, Ca, 2] (+ stats_b [B, C - Ca, 2] for a
+// channel concatenation), as accumulated by gemm/conv2d(stats=...)
+void group_norm_stats(const at::Tensor& x, const at::Tensor& stats_a, const c10::optional<at::Tensor>& stats_b,
+                      const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& out, int64_t groups, double eps,
+                      int64_t silu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(gamma); CHECK_BF16(beta); CHECK_CONTIG(out);
+  const int B = (int)x.size(0);
+  const int C = (int)x.size(-1);
+  const long long S = x.numel() / ((long long)B * C);
+  TORCH_CHECK(C % 8 == 0 && C % groups == 0, "group_norm_stats: C must be a multiple of 8 and of groups");
+  TORCH_CHECK(stats_a.scalar_type() == at::kFloat && stats_a.is_contiguous() && stats_a.dim() == 3 &&
+              stats_a.size(0) == B && stats_a.size(2) == 2, "group_norm_stats: stats_a must be fp32 [B, Ca, 2]");
+  const int Ca = (int)stats_a.size(1);
+  const float* sb = nullptr;
+  if (stats_b.has_value() && stats_b->defined()) {
+    TORCH_CHECK(stats_b->scalar_type() == at::kFloat && stats_b->is_contiguous() && stats_b->dim() == 3 &&
+                stats_b->size(0) == B && stats_b->size(1) == C - Ca && stats_b->size(2) == 2,
+                "group_norm_stats: stats_b must be fp32 [B, C - Ca, 2]");
+    sb = stats_b->data_ptr<float>();
+  } else {
+    TORCH_CHECK(Ca == C, "group_norm_stats: stats_a must cover every channel");
+  }
+  launch_group_norm_cs(bptr(x), stats_a.data_ptr<float>(), Ca, sb, bptr(gamma), bptr(beta), bptr_mut(out), B, S, C,
+                       (int)groups, (float)eps, (int)silu, cur_stream());
+}
+
+void channel_stats(const at::Tensor& x, at::Tensor& stats) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int B = (int)x.size(0);
+  const int C = (int)x.size(-1);
+  const long long S = x.numel() / ((long long)B * C);
+  TORCH_CHECK(C % 8 == 0, "channel_stats: C % 8 == 0");
+  launch_channel_stats(bptr(x), opt_stats(stats, B, C), B, S, C, cur_stream());
 }
 
 void layer_norm(const at::Tensor& x, const at::Tensor& gamma, const c10::optional<at::Tensor>& beta, at::Tensor& out,
@@ -351,6 +416,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bmm_nt", &bmm_nt);
   m.def("group_norm", &group_norm);
   m.def("layer_norm", &layer_norm);
+  m.def("group_norm_stats", &group_norm_stats);
+  m.def("channel_stats", &channel_stats);
   m.def("attention", &attention);
   m.def("gather_cosine", &gather_cosine);
   m.def("pair_cosine", &pair_cosine);

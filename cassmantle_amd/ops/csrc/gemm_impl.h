@@ -25,6 +25,8 @@
 // * Split-K: grids that cannot fill the 256 CUs (the 16x16 / 8x8 UNet levels: M = 2048 / 512
 //   with K = 11520) split the k-tiles over blockIdx.y; fp32 partial slabs are summed by a
 //   second kernel that applies the epilogue (cheaper than a sub-occupied chip).
+// * GroupNorm statistics of the output (p.stats) are accumulated in the epilogue, so a
+//   following GroupNorm needs no statistics pass over the activation.
 // * GEGLU (transformer FF): W tile rows interleave 16-row value/gate blocks, so each lane
 //   holds h and g of the same output column and computes h * gelu(g) in registers.
 // * Block ids are remapped XCD-aware so tiles that share an A panel run on one XCD's L2.
@@ -451,10 +453,8 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       __syncthreads();
       constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
       uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
-      for (int c = tid; c < BM * CPR; c += THREADS) {
-        const int row = c / CPR, c8 = c - row * CPR;
+      auto finish = [&](int row, int c8) -> uint4 {   // residual add + store of one 16-B chunk
         const int m = m0 + row, n = n0 + c8 * 8;
-        if (m >= p.M || n >= p.N) continue;
         uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
         if (p.residual) {
           const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + (long long)m * p.ldc + n);
@@ -466,6 +466,77 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
           v = pack8(a);
         }
         *reinterpret_cast<uint4*>(Cb + (long long)m * p.ldc + n) = v;
+        return v;
+      };
+      if (p.stats == nullptr) {
+        for (int c = tid; c < BM * CPR; c += THREADS) {
+          const int row = c / CPR, c8 = c - row * CPR;
+          if (m0 + row >= p.M || n0 + c8 * 8 >= p.N) continue;
+          finish(row, c8);
+        }
+        return;
+      }
+      // GroupNorm statistics of the stored output (consumer: group_norm with stats): each thread
+      // owns one 8-column chunk and walks rows; per-(image, column) sum / sum-of-squares are
+      // reduced over the row lanes in LDS and added to p.stats[image][n][2] with one atomic per
+      // column per tile (tiles that straddle images flush per thread instead).
+      constexpr int RL = THREADS / CPR;          // row lanes
+      const int c8 = tid % CPR, r0 = tid / CPR;
+      const int n = n0 + c8 * 8;
+      const bool lane_on = r0 < RL && n < p.N;
+      const int shw = p.stats_hw;
+      const int mlast = min(m0 + BM, p.M) - 1;
+      const int img0 = m0 / shw;
+      const bool single = img0 == mlast / shw;
+      float s8[8], q8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
+      int cur = -1;
+      auto flush = [&]() {
+        if (cur < 0) return;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, s8[e]);
+          atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, q8[e]);
+          s8[e] = 0.f;
+          q8[e] = 0.f;
+        }
+      };
+      if (lane_on) {
+        for (int row = r0; row < BM; row += RL) {
+          const int m = m0 + row;
+          if (m >= p.M) break;
+          const uint4 v = finish(row, c8);
+          if (!single) {
+            const int img = m / shw;
+            if (img != cur) { flush(); cur = img; }
+          }
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s8[e] += f[e]; q8[e] = fmaf(f[e], f[e], q8[e]); }
+        }
+      }
+      if (!single) {
+        flush();
+        return;
+      }
+      __syncthreads();                          // T fully consumed: reuse LDS for the reduction
+      float* R = reinterpret_cast<float*>(smem);   // [2][RL][OBN]
+      if (r0 < RL) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          R[r0 * OBN + c8 * 8 + e] = s8[e];
+          R[(RL + r0) * OBN + c8 * 8 + e] = q8[e];
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < 2 * OBN; c += THREADS) {
+        const int stat = c / OBN, col = c - stat * OBN;
+        if (n0 + col >= p.N) continue;
+        float a = 0.f;
+        for (int r = 0; r < RL; ++r) a += R[(stat * RL + r) * OBN + col];
+        atomicAdd(p.stats + ((long long)img0 * p.N + n0 + col) * 2 + stat, a);
       }
       return;
     }
@@ -509,6 +580,9 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   }
 }
 
+// split-K: a second, fully parallel pass sums the slices' fp32 slabs and applies the epilogue
+// (an in-kernel last-arriver reduction was measured 1.3-2.4x slower on the split shapes: one
+// block serially reading up to 15 slabs of its tile)
 template <bool OUTF32>
 __global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ partial, int split) {
   const long long nq = (long long)p.M * (p.N / 4);

@@ -26,6 +26,10 @@ struct GemmArgs {
   // fused RMSNorm of A's rows (GEMV path only): A <- A * gamma / rms(A)
   const uint16_t* rms_gamma = nullptr;
   float rms_eps = 0.f;
+  // GroupNorm statistics of the output: atomically accumulated per-(image, column) sum and
+  // sum-of-squares [M / stats_hw][N][2] fp32 (zeroed by the caller); stats_hw = rows per image
+  float* stats = nullptr;
+  int stats_hw = 0;
 };
 #define GEMM_MAX_SPLIT 16
 struct GemmPlan { int cfg; int split; };
@@ -54,6 +58,13 @@ void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s)
 // norms
 void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        float* ws, int B, long long S, int C, int G, float eps, int silu, hipStream_t s);
+// GroupNorm from producer-accumulated per-channel stats ([B][Ca][2] for channels < Ca, then
+// [B][C-Ca][2] from stats_b when the input is a channel concatenation); no statistics pass
+void launch_group_norm_cs(const uint16_t* x, const float* stats_a, int Ca, const float* stats_b,
+                          const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
+                          int G, float eps, int silu, hipStream_t s);
+// per-channel stats of an NHWC tensor into zeroed [B][C][2] (for producers without a fused path)
+void launch_channel_stats(const uint16_t* x, float* stats, int B, long long S, int C, hipStream_t s);
 long long group_norm_workspace(int B, long long S, int C);
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        long long rows, int D, float eps, hipStream_t s);

@@ -206,6 +206,151 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __
       if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(xb + r * C + (tv + T * j) * 8));
 }
 
+// GroupNorm apply from producer-accumulated per-channel statistics (GEMM epilogue, p.stats):
+// each block first folds the Cg channel sums of every group of its image into (mean, rstd) in
+// LDS (fp64), then streams rows exactly like gn_apply_kernel.  A channel concatenation
+// (UNet up-block skips) reads channels >= Ca from the second producer's statistics.
+template <int VPT>
+__global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t* __restrict__ x,
+                                                                 const float* __restrict__ sa, int Ca,
+                                                                 const float* __restrict__ sb,
+                                                                 const uint16_t* __restrict__ gamma,
+                                                                 const uint16_t* __restrict__ beta,
+                                                                 uint16_t* __restrict__ y, long long S, int C,
+                                                                 int G, int T, int R, long long rows_per_block,
+                                                                 float eps, int silu) {
+  extern __shared__ float gst[];           // [G][2] mean, rstd, then [C][2] channel sums
+  const int V = C / 8;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int Cg = C / G;
+  const int Cb = C - Ca;
+  // channel (sum, sumsq) pairs -> LDS with one coalesced pass (all loads in flight at once: a
+  // per-group serial walk of Cg dependent L2 loads cost ~Cg x 0.2 us in every block), then one
+  // thread per group folds its Cg channels from LDS in fp64
+  float2* cst = reinterpret_cast<float2*>(gst + 2 * G);
+  for (int c = tid; c < C; c += GN_THREADS)
+    cst[c] = c < Ca ? *reinterpret_cast<const float2*>(sa + ((long long)b * Ca + c) * 2)
+                    : *reinterpret_cast<const float2*>(sb + ((long long)b * Cb + (c - Ca)) * 2);
+  __syncthreads();
+  for (int g = tid; g < G; g += GN_THREADS) {
+    double s = 0.0, q = 0.0;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      const float2 v = cst[c];
+      s += v.x;
+      q += v.y;
+    }
+    const double n = (double)S * Cg;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    gst[2 * g] = (float)mean;
+    gst[2 * g + 1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  const int tv = tid % T, rl = tid / T;
+  if (rl >= R) return;
+  float sc[VPT][8], sf[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int v = tv + T * j;
+    if (v >= V) continue;
+    float ga[8], be[8];
+    unpack8(*reinterpret_cast<const uint4*>(gamma + v * 8), ga);
+    unpack8(*reinterpret_cast<const uint4*>(beta + v * 8), be);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int g = (v * 8 + i) / Cg;
+      sc[j][i] = ga[i] * gst[2 * g + 1];
+      sf[j][i] = be[i] - gst[2 * g] * sc[j][i];
+    }
+  }
+  const long long rbeg = (long long)blockIdx.x * rows_per_block;
+  const long long rend = min(S, rbeg + rows_per_block);
+  const long long off = (long long)b * S * C;
+  const uint16_t* xb = x + off;
+  uint16_t* yb = y + off;
+  auto emit = [&](long long r, int j, uint4 u) {
+    float f[8];
+    unpack8(u, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float o = fmaf(f[i], sc[j][i], sf[j][i]);
+      f[i] = silu ? silu_f(o) : o;
+    }
+    *reinterpret_cast<uint4*>(yb + r * C + (tv + T * j) * 8) = pack8(f);
+  };
+  long long r = rbeg + rl;
+  for (; r + (GN_UNROLL - 1) * R < rend; r += GN_UNROLL * R) {
+    uint4 u[GN_UNROLL][VPT];
+#pragma unroll
+    for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = tv + T * j;
+        if (v < V) u[k][j] = *reinterpret_cast<const uint4*>(xb + (r + (long long)k * R) * C + v * 8);
+      }
+#pragma unroll
+    for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+        if (tv + T * j < V) emit(r + (long long)k * R, j, u[k][j]);
+  }
+  for (; r < rend; r += R)
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+      if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(xb + r * C + (tv + T * j) * 8));
+}
+
+// per-channel sum / sum-of-squares of an NHWC tensor, atomically added into [B][C][2]
+template <int VPT>
+__global__ void __launch_bounds__(GN_THREADS) channel_stats_kernel(const uint16_t* __restrict__ x,
+                                                                   float* __restrict__ stats, long long S, int C,
+                                                                   int T, int R, long long rows_per_chunk) {
+  extern __shared__ float sh[];              // [2][R][C]
+  const int V = C / 8;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const long long rbeg = (long long)blockIdx.x * rows_per_chunk;
+  const long long rend = min(S, rbeg + rows_per_chunk);
+  const uint16_t* base = x + (long long)b * S * C;
+  const int tv = tid % T, rl = tid / T;
+  float s[VPT][8], q[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s[j][i] = 0.f; q[j][i] = 0.f; }
+  if (rl < R) {
+    for (long long r = rbeg + rl; r < rend; r += R)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = tv + T * j;
+        if (v >= V) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(base + r * C + v * 8), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s[j][i] += f[i]; q[j][i] = fmaf(f[i], f[i], q[j][i]); }
+      }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = tv + T * j;
+      if (v >= V) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sh[(long long)rl * C + v * 8 + i] = s[j][i];
+        sh[(long long)(R + rl) * C + v * 8 + i] = q[j][i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < 2 * C; c += GN_THREADS) {
+    const int stat = c / C, ch = c - stat * C;
+    float acc = 0.f;
+    for (int k = 0; k < R; ++k) acc += sh[(long long)(stat * R + k) * C + ch];
+    atomicAdd(stats + ((long long)b * C + ch) * 2 + stat, acc);
+  }
+}
+
 // LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): T lanes per row, VPL vectors per lane
 template <int VPL, bool RMS>
 __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gamma,
@@ -307,6 +452,39 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
   else
     hipLaunchKernelGGL(gn_apply_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), 0, s, x, stats, gamma, beta, y, S,
                        C, G, g.T, g.R, rpb, silu);
+}
+
+void launch_group_norm_cs(const uint16_t* x, const float* stats_a, int Ca, const float* stats_b,
+                          const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
+                          int G, float eps, int silu, hipStream_t s) {
+  const GnGeom g = gn_geom(C);
+  long long rpb = 8LL * g.R;
+  long long nb = (S + rpb - 1) / rpb;
+  if (nb * B < 1024) {
+    rpb = (long long)g.R * 2;
+    nb = (S + rpb - 1) / rpb;
+  }
+  const size_t shs = sizeof(float) * 2 * (G + C);
+  if (stats_b == nullptr) Ca = C;
+  if (g.VPT == 1)
+    hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, stats_a, Ca,
+                       stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
+  else
+    hipLaunchKernelGGL(gn_apply_cs_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, stats_a, Ca,
+                       stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
+}
+
+void launch_channel_stats(const uint16_t* x, float* stats, int B, long long S, int C, hipStream_t s) {
+  const GnGeom g = gn_geom(C);
+  const int chunks = gn_chunks(B, S, g.R);
+  const long long rpc = (S + chunks - 1) / chunks;
+  const size_t shs = sizeof(float) * 2LL * g.R * C;
+  if (g.VPT == 1)
+    hipLaunchKernelGGL(channel_stats_kernel<1>, dim3(chunks, B), dim3(GN_THREADS), shs, s, x, stats, S, C, g.T, g.R,
+                       rpc);
+  else
+    hipLaunchKernelGGL(channel_stats_kernel<2>, dim3(chunks, B), dim3(GN_THREADS), shs, s, x, stats, S, C, g.T, g.R,
+                       rpc);
 }
 
 template <int VPL, bool RMS>

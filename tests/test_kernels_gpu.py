@@ -120,6 +120,47 @@ def test_group_norm(shape, G, silu, eps):
     assert rel_err(out, exp) < 1e-2
 
 
+@pytest.mark.parametrize("kind,B,H,Cin,Cout", [
+    ("conv", 2, 16, 64, 128),       # single-image tiles
+    ("conv", 8, 8, 128, 320),       # 64-pixel images: tiles straddle images (per-thread flush)
+    ("conv", 2, 8, 1280, 1280),     # split-K grid: statistics in the last slice's epilogue
+    ("linear", 2, 32, 320, 320),
+    ("linear", 1, 2, 64, 96),       # 4 rows: GEMV path + separate statistics pass
+])
+def test_epilogue_group_norm_statistics(kind, B, H, Cin, Cout):
+    """GEMM/conv epilogue statistics (sum, sum of squares per image and channel) feeding the
+    apply-only GroupNorm must equal the plain two-pass GroupNorm of the same tensor."""
+    x = rnd(B, H, H, Cin, seed=50) + 0.25
+    st = torch.zeros(B, Cout, 2, device=DEV)
+    if kind == "conv":
+        w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=51)
+        y = ops.conv2d(x, w, rnd(Cout, scale=0.3, seed=52), stats=st)
+    else:
+        w = rnd(Cout, Cin, scale=Cin ** -0.5, seed=51)
+        y = ops.linear(x, w, rnd(Cout, scale=0.3, seed=52), residual=rnd(B, H, H, Cout, seed=53), stats=st)
+    exp_st = torch.zeros_like(st)
+    ops.channel_stats_ref(y, exp_st)
+    assert rel_err(st, exp_st) < 1e-4
+    G = 32 if Cout % 32 == 0 else 4
+    g = rnd(Cout, seed=54) * 0.5 + 1
+    b = rnd(Cout, seed=55) * 0.1
+    out = ops.group_norm(y, G, g, b, 1e-5, True, stats=st)
+    assert rel_err(out, ref.group_norm(y, G, g, b, 1e-5, True)) < 1e-2
+
+
+def test_group_norm_statistics_of_a_concatenation():
+    a = rnd(2, 16, 16, 640, seed=56) + 0.5
+    s = rnd(2, 16, 16, 320, seed=57) - 0.25
+    sa, sb = torch.zeros(2, 640, 2, device=DEV), torch.zeros(2, 320, 2, device=DEV)
+    ops.channel_stats(a, sa)
+    ops.channel_stats(s, sb)
+    x = torch.cat([a, s], dim=-1)
+    g = rnd(960, seed=58) * 0.5 + 1
+    b = rnd(960, seed=59) * 0.1
+    out = ops.group_norm(x, 32, g, b, 1e-5, True, stats=sa, stats2=sb)
+    assert rel_err(out, ref.group_norm(x, 32, g, b, 1e-5, True)) < 1e-2
+
+
 @pytest.mark.parametrize("D,rows", [(320, 333), (384, 333), (768, 333), (1280, 333), (32, 333), (640, 1),
                                     (4096, 7), (136, 45)])
 def test_layer_norm(D, rows):
