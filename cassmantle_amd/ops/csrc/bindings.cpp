@@ -38,15 +38,15 @@ float* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N) {
 
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
   // output statistics are fused into the LDS-staged bf16 epilogue; shapes that take another
-  // path (fp32 out, GEMV rows, batched, gated, split-K reduce pass) get a separate per-channel
-  // statistics pass over the output
+  // path (fp32 out, GEMV rows, batched, gated) get a separate per-channel statistics pass over
+  // the output; split-K shapes accumulate them in the reduce pass
   TORCH_CHECK(p.stats == nullptr || (p.N % 8 == 0 && p.ldc == p.N),
               "gemm/conv2d stats: the output channel count must be a multiple of 8 (GroupNorm consumers)");
   const GemmPlan plan = gemm_plan(p);
   p.cfg = plan.cfg;
   p.split = plan.split;
   float* post_stats = nullptr;
-  if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || p.batch != 1 || p.split > 1 || p.act == 4 || p.act == 6)) {
+  if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || p.batch != 1 || p.act == 4 || p.act == 6)) {
     post_stats = p.stats;
     p.stats = nullptr;
   }

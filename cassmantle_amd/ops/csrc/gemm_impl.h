@@ -598,6 +598,75 @@ __global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ parti
   }
 }
 
+// split-K reduce + GroupNorm statistics of the output (p.stats): block = 64 column quads x 4
+// row lanes over RB rows; each thread sums the slabs of its quad for RB/4 rows, runs the
+// epilogue, and accumulates (sum, sumsq) of the stored bf16 values; the 4 row lanes are folded
+// in LDS and added with one atomic per (column, statistic) per block (per-thread flushes when a
+// block's rows straddle images)
+constexpr int SK_RB = 32;
+template <bool OUTF32>
+__global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, const float* __restrict__ partial,
+                                                                  int split) {
+  __shared__ float red[2][4][256];
+  const int qd = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = (blockIdx.x * 64 + qd) * 4;
+  const int m0 = blockIdx.y * SK_RB;
+  const int m1 = min(p.M, m0 + SK_RB);
+  const bool on = n < p.N;
+  const int shw = p.stats_hw;
+  const bool single = (m0 / shw) == ((m1 - 1) / shw);
+  float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, s4[e]);
+      atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, q4[e]);
+      s4[e] = 0.f;
+      q4[e] = 0.f;
+    }
+  };
+  if (on) {
+    for (int m = m0 + rl; m < m1; m += 4) {
+      float o[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < split; ++sl) {
+        const float4 v = *reinterpret_cast<const float4*>(partial + ((long long)sl * p.M + m) * p.N + n);
+        o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
+      }
+      epilogue4<OUTF32>(p, 0, m, n, o);      // (N % 8 == 0: o holds the final values)
+      if (!single) {
+        const int img = m / shw;
+        if (img != cur) { flush(); cur = img; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float f = OUTF32 ? o[e] : bf2f(f2bf(o[e]));
+        s4[e] += f;
+        q4[e] = fmaf(f, f, q4[e]);
+      }
+    }
+  }
+  if (!single) {
+    flush();
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][rl][qd * 4 + e] = s4[e];
+    red[1][rl][qd * 4 + e] = q4[e];
+  }
+  __syncthreads();
+  const int img = m0 / shw;
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int st = c >> 8, col = c & 255;
+    const int nn = blockIdx.x * 256 + col;
+    if (nn >= p.N) continue;
+    const float a = red[st][0][col] + red[st][1][col] + red[st][2][col] + red[st][3][col];
+    atomicAdd(p.stats + ((long long)img * p.N + nn) * 2 + st, a);
+  }
+}
+
 int g_stages_override = -1;   // CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark)
 
 int stages_pref() {
@@ -629,7 +698,10 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
     }
   }
   hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * WN), lds, s, p, ws);
-  if (split > 1) {
+  if (split > 1 && p.stats != nullptr) {
+    dim3 g2((unsigned)((p.N / 4 + 63) / 64), (unsigned)((p.M + SK_RB - 1) / SK_RB));
+    hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split);
+  } else if (split > 1) {
     const long long nq = (long long)p.M * (p.N / 4);
     const long long nb = (nq + 255) / 256;
     const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);

@@ -123,7 +123,10 @@ def test_group_norm(shape, G, silu, eps):
 @pytest.mark.parametrize("kind,B,H,Cin,Cout", [
     ("conv", 2, 16, 64, 128),       # single-image tiles
     ("conv", 8, 8, 128, 320),       # 64-pixel images: tiles straddle images (per-thread flush)
-    ("conv", 2, 8, 1280, 1280),     # split-K grid: statistics in the last slice's epilogue
+    ("conv", 2, 8, 1280, 1280),     # split-K grid: statistics in the reduce pass
+    ("conv", 8, 16, 1280, 1280),    # UNet 16x16 level (split-K)
+    ("conv", 8, 8, 1280, 1280),     # UNet 8x8 level (split-K, 64-pixel images)
+    ("conv", 4, 6, 640, 640),       # 36-pixel images: reduce blocks straddle images
     ("linear", 2, 32, 320, 320),
     ("linear", 1, 2, 64, 96),       # 4 rows: GEMV path + separate statistics pass
 ])
