@@ -411,6 +411,7 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
   m.def("gemm", &gemm);
+  m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });
   m.def("gemm_rms", &gemm_rms);
   m.def("conv2d", &conv2d);
   m.def("bmm_nt", &bmm_nt);

@@ -98,11 +98,21 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// A/B knobs for the microbenchmark / tile sweeps: CASSMANTLE_GEMM_CFG=<tile index>,
+// CASSMANTLE_GEMM_SPLIT=<k slices>, or at run time gemm_set_override (tools/sweep_gemm.py)
+static int g_force_cfg = -2, g_force_split = 0;   // -2: not yet read from the environment
+void gemm_set_override(int cfg, int split) {
+  g_force_cfg = cfg;
+  g_force_split = split;
+}
+
 GemmPlan gemm_plan(const GemmArgs& p) {
   GemmPlan best{0, 1};
-  // A/B knobs for the microbenchmark: CASSMANTLE_GEMM_CFG=<tile index>, CASSMANTLE_GEMM_SPLIT=<k slices>
-  static const int force_cfg = env_int("CASSMANTLE_GEMM_CFG", -1);
-  static const int force_split = env_int("CASSMANTLE_GEMM_SPLIT", 0);
+  if (g_force_cfg == -2) {
+    g_force_cfg = env_int("CASSMANTLE_GEMM_CFG", -1);
+    g_force_split = env_int("CASSMANTLE_GEMM_SPLIT", 0);
+  }
+  const int force_cfg = g_force_cfg, force_split = g_force_split;
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
   const bool gated = p.act == ACT_GEGLU || p.act == ACT_SWIGLU;
   int only = -1;                         // forced tile (cost model still picks the split)

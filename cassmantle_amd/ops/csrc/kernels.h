@@ -35,6 +35,8 @@ struct GemmArgs {
 struct GemmPlan { int cfg; int split; };
 GemmPlan gemm_plan(const GemmArgs& p);
 int gemm_plan_split(const GemmArgs& p);
+// force a tile config (-1: cost model) and split-K factor (0: cost model) for every later plan
+void gemm_set_override(int cfg, int split);
 // ws: fp32 workspace of split * M * N floats when split > 1 (else may be null)
 void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s);
 
