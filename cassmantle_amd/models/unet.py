@@ -71,11 +71,18 @@ class ResnetBlock(nn.Module):
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0, gen=gen, dtype=dtype) if cin != cout else None
 
     def forward(self, x, temb_silu, tb_all=None, arena: Optional[StatsArena] = None, xs=None, xs2=None):
-        """``xs`` / ``xs2``: epilogue statistics of x (of its two halves for an up-block skip
-        concatenation).  Returns (out, statistics of out or None)."""
-        B = x.shape[0]
+        """``x``: a tensor, or for an up-block a pair (h, skip) standing for their channel
+        concatenation, which is never materialised (the GroupNorm reads both, the 1x1 shortcut
+        GEMM stages its k-tiles from both).  ``xs`` / ``xs2``: epilogue statistics of x (of the two
+        halves of a pair).  Returns (out, statistics of out or None)."""
+        pair = isinstance(x, tuple)
+        B = x[0].shape[0] if pair else x.shape[0]
         cout = self.conv1.cout
-        h = self.norm1(x, silu=True, stats=xs, stats2=xs2)
+        if pair:
+            g = self.norm1
+            h = ops.group_norm_cat(x[0], x[1], g.groups, g.weight, g.bias, g.eps, True, stats=xs, stats2=xs2)
+        else:
+            h = self.norm1(x, silu=True, stats=xs, stats2=xs2)
         if tb_all is not None:                                   # slice of the UNet-wide batched GEMM
             tb = tb_all[:, self._tb_off:self._tb_off + self.time_emb_proj.fout]
         else:
@@ -83,7 +90,13 @@ class ResnetBlock(nn.Module):
         s1 = arena.take(B, cout) if arena is not None else None
         h = self.conv1(h, chan_bias=tb, stats=s1)                # time-emb add fused in epilogue
         h = self.norm2(h, silu=True, stats=s1)                   # statistics from conv1's epilogue
-        sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        if pair and self.conv_shortcut is None:
+            sc = torch.cat(x, dim=-1)
+        elif pair:
+            cs = self.conv_shortcut
+            sc = ops.linear_cat(x[0], x[1], cs.weight.view(cs.cout, cs.cin), cs.bias)
+        else:
+            sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
         s2 = arena.take(B, cout) if arena is not None else None
         return self.conv2(h, residual=sc, stats=s2), s2          # residual fused in epilogue
 
@@ -262,13 +275,34 @@ class UNet(nn.Module):
         for m in ca:
             m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
 
-    def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor,
-                added: Optional[dict] = None, fp8: bool = False) -> torch.Tensor:
-        """x [B, H, W, 4] NHWC, t [B] (float), ctx [B, 77, D] -> eps [B, H, W, 4]."""
+    def time_table(self, tsteps: torch.Tensor, nb: int, added: Optional[dict] = None):
+        """Time conditioning of a whole denoise schedule at once: SiLU(temb) [E, nb, D] and every
+        ResNet's time bias [E, nb, sum Cout] for the E timesteps of a plan.  Both depend only on
+        (t, add-embeds), so a sampler computes them with ONE batched MLP + GEMM per generation
+        (E*nb rows) instead of the time MLP and an M=nb weight-streaming GEMV in every step."""
         if not getattr(self, "_fused", False):
             self.fuse_projections()
-        temb = self.time_embed(t, added)
-        tb = ops.linear(temb, self._tb_w, self._tb_b)               # all ResNets' time biases
+        E = tsteps.shape[0]
+        t = tsteps.float().repeat_interleave(nb)                     # row e*nb + b <- tsteps[e]
+        rep = None
+        if added is not None:
+            rep = {k: v.repeat(E, *([1] * (v.dim() - 1))) for k, v in added.items()}
+        temb = self.time_embed(t, rep)
+        tb = ops.linear(temb, self._tb_w, self._tb_b)
+        return temb.view(E, nb, -1), tb.view(E, nb, -1)
+
+    def forward(self, x: torch.Tensor, t: Optional[torch.Tensor], ctx: torch.Tensor,
+                added: Optional[dict] = None, fp8: bool = False, time_cond=None) -> torch.Tensor:
+        """x [B, H, W, 4] NHWC, t [B] (float), ctx [B, 77, D] -> eps [B, H, W, 4].
+        ``time_cond``: (SiLU(temb) [B, D], time biases [B, sum Cout]) rows of :meth:`time_table`
+        (then ``t`` / ``added`` are not used for the time embedding)."""
+        if not getattr(self, "_fused", False):
+            self.fuse_projections()
+        if time_cond is not None:
+            temb, tb = time_cond
+        else:
+            temb = self.time_embed(t, added)
+            tb = ops.linear(temb, self._tb_w, self._tb_b)           # all ResNets' time biases
         # every producer of a GroupNorm input (conv_in, ResNet conv1/conv2, transformer
         # proj_out, down/up-sample convs) accumulates the output statistics in its epilogue,
         # so the 61 GroupNorms of a step run their apply pass only
@@ -292,10 +326,10 @@ class UNet(nn.Module):
         for blk in self.up:
             for j, res in enumerate(blk.resnets):
                 sk, sks = skips.pop()
-                h = torch.cat([h, sk], dim=-1)
-                # statistics of the concatenation = (statistics of h, statistics of the skip)
+                # [h | skip] is passed as a pair: never concatenated in memory; its statistics
+                # are (statistics of h, statistics of the skip)
                 two = hs is not None and sks is not None
-                h, hs = res(h, temb, tb, ar, hs if two else None, sks if two else None)
+                h, hs = res((h, sk), temb, tb, ar, hs if two else None, sks if two else None)
                 if len(blk.attentions):
                     h, hs = blk.attentions[j](h, ctx, fp8, ar, hs)
             if blk.upsampler is not None:

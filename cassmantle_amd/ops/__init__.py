@@ -93,6 +93,24 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out.reshape(*x.shape[:-1], N)
 
 
+def linear_cat(x: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+               residual: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear(cat([x, x2], -1), w, bias, residual)`` without materialising the concatenation
+    (UNet up-block ResNet shortcut over [h | skip]).  The HIP GEMM stages k-tiles < Ca from x and
+    the rest from x2; shapes it does not take (Ca or K not multiples of 64, <= 8 rows) and the
+    CPU / torch paths concatenate."""
+    Ca, K = x.shape[-1], x.shape[-1] + x2.shape[-1]
+    rows = x.numel() // Ca
+    if not _use_hip(x) or Ca % 64 or K % 64 or rows <= 8:
+        return linear(torch.cat([x, x2], dim=-1), w, bias, residual=residual, stats=stats)
+    N = w.shape[0]
+    out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
+    r2 = residual.reshape(rows, N) if residual is not None else None
+    hw = rows // x.shape[0] if stats is not None else 0
+    ext().gemm_cat(x.reshape(rows, Ca).contiguous(), x2.reshape(rows, K - Ca).contiguous(), w, bias, r2, out, stats, hw)
+    return out.reshape(*x.shape[:-1], N)
+
+
 def _torch_linear(x, w, bias, residual, act):
     import torch.nn.functional as F
     y = F.linear(x, w, bias)
@@ -206,6 +224,20 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: torch.Tensor, bias: tor
         return ref.group_norm(x, num_groups, weight, bias, eps, silu)
     out = torch.empty_like(x)
     ext().group_norm(x.contiguous(), weight, bias, out, num_groups, float(eps), int(silu))
+    return out
+
+
+def group_norm_cat(x: torch.Tensor, x2: torch.Tensor, num_groups: int, weight: torch.Tensor, bias: torch.Tensor,
+                   eps: float, silu: bool = False, stats: Optional[torch.Tensor] = None,
+                   stats2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``group_norm(cat([x, x2], -1), ...)``: with both producers' statistics the HIP kernel reads
+    the two tensors directly and writes the normalised concatenation (the raw concatenation is
+    never materialised); otherwise it concatenates first."""
+    if stats is None or stats2 is None or not _use_hip(x) or x.shape[-1] % 8 or x2.shape[-1] % 8:
+        return group_norm(torch.cat([x, x2], dim=-1), num_groups, weight, bias, eps, silu, stats=stats, stats2=stats2)
+    out = torch.empty((*x.shape[:-1], x.shape[-1] + x2.shape[-1]), device=x.device, dtype=x.dtype)
+    ext().group_norm_cat(x.contiguous(), x2.contiguous(), stats, stats2, weight, bias, out, num_groups, float(eps),
+                         int(silu))
     return out
 
 

@@ -93,6 +93,35 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   run_gemm(p, out);
 }
 
+// y = [x | x2] @ w^T + bias (+ residual, + output statistics) without materialising the channel
+// concatenation: the GEMM stages k-tiles < Ca from x and the rest from x2 (UNet up-block
+// ResNet shortcut over [h | skip]); Ca and K multiples of 64, M > 8
+void gemm_cat(const at::Tensor& x, const at::Tensor& x2, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+              const c10::optional<at::Tensor>& residual, at::Tensor& out, const c10::optional<at::Tensor>& stats,
+              int64_t stats_hw) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_BF16(w); CHECK_CONTIG(w);
+  CHECK_BF16(out); CHECK_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && x2.dim() == 2 && w.dim() == 2 && out.dim() == 2 && x.size(0) == x2.size(0),
+              "gemm_cat: 2-D operands with equal rows expected");
+  GemmArgs p;
+  p.A = bptr(x); p.A2 = bptr(x2); p.W = bptr(w); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
+  p.M = (int)x.size(0); p.ka = (int)x.size(1); p.K = p.ka + (int)x2.size(1);
+  p.N = (int)out.size(1); p.Nw = (int)w.size(0);
+  p.lda = p.ka; p.lda2 = (int)x2.size(1); p.ldc = p.N;
+  TORCH_CHECK(w.size(1) == p.K && p.Nw == p.N && out.size(0) == p.M, "gemm_cat: shape mismatch");
+  TORCH_CHECK(p.ka % 64 == 0 && p.K % 64 == 0 && p.M > 8, "gemm_cat: Ca and K must be multiples of 64, M > 8");
+  const long long lim = (1LL << 31) - 1;
+  TORCH_CHECK(x.numel() * 2 <= lim && x2.numel() * 2 <= lim && w.numel() * 2 <= lim, "gemm_cat: operand too large");
+  if (residual.has_value() && residual->defined()) TORCH_CHECK(residual->numel() == out.numel(), "gemm_cat: residual shape");
+  p.C = out.data_ptr();
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats_hw > 0 && p.M % stats_hw == 0, "gemm_cat: stats_hw must divide the rows");
+    p.stats_hw = (int)stats_hw;
+    p.stats = opt_stats(stats, p.M / stats_hw, p.N);
+  }
+  run_gemm(p, out);
+}
+
 // y = act(rmsnorm(x) @ w^T + bias) + residual for skinny x (<= 8 rows): the norm is fused into
 // the weight-streaming GEMV (decode path of the causal LM)
 void gemm_rms(const at::Tensor& x, const at::Tensor& gamma, double eps, const at::Tensor& w,
@@ -203,8 +232,29 @@ void group_norm_stats(const at::Tensor& x, const at::Tensor& stats_a, const c10:
   } else {
     TORCH_CHECK(Ca == C, "group_norm_stats: stats_a must cover every channel");
   }
-  launch_group_norm_cs(bptr(x), stats_a.data_ptr<float>(), Ca, sb, bptr(gamma), bptr(beta), bptr_mut(out), B, S, C,
+  launch_group_norm_cs(bptr(x), nullptr, stats_a.data_ptr<float>(), Ca, sb, bptr(gamma), bptr(beta), bptr_mut(out), B, S, C,
                        (int)groups, (float)eps, (int)silu, cur_stream());
+}
+
+// GroupNorm(+SiLU) of the channel concatenation [x | x2] (NHWC, same B and pixels) from the
+// producers' statistics, written as one contiguous [.., Ca + Cb] output; the concatenation
+// itself is never materialised
+void group_norm_cat(const at::Tensor& x, const at::Tensor& x2, const at::Tensor& stats_a, const at::Tensor& stats_b,
+                    const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& out, int64_t groups, double eps,
+                    int64_t silu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_BF16(gamma); CHECK_BF16(beta);
+  CHECK_CONTIG(out); CHECK_BF16(out);
+  const int B = (int)x.size(0);
+  const int Ca = (int)x.size(-1), Cb = (int)x2.size(-1), C = Ca + Cb;
+  const long long S = x.numel() / ((long long)B * Ca);
+  TORCH_CHECK(x2.size(0) == B && x2.numel() == (long long)B * S * Cb && out.numel() == (long long)B * S * C &&
+              out.size(-1) == C, "group_norm_cat: shapes must agree on batch and pixels");
+  TORCH_CHECK(Ca % 8 == 0 && Cb % 8 == 0 && C % groups == 0, "group_norm_cat: channel counts");
+  TORCH_CHECK(stats_a.scalar_type() == at::kFloat && stats_a.is_contiguous() && stats_a.numel() == (long long)B * Ca * 2 &&
+              stats_b.scalar_type() == at::kFloat && stats_b.is_contiguous() && stats_b.numel() == (long long)B * Cb * 2,
+              "group_norm_cat: fp32 [B, C, 2] statistics of both inputs expected");
+  launch_group_norm_cs(bptr(x), bptr(x2), stats_a.data_ptr<float>(), Ca, stats_b.data_ptr<float>(), bptr(gamma),
+                       bptr(beta), bptr_mut(out), B, S, C, (int)groups, (float)eps, (int)silu, cur_stream());
 }
 
 void channel_stats(const at::Tensor& x, at::Tensor& stats) {
@@ -411,6 +461,8 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
   m.def("gemm", &gemm);
+  m.def("gemm_cat", &gemm_cat);
+  m.def("group_norm_cat", &group_norm_cat);
   m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });
   m.def("gemm_rms", &gemm_rms);
   m.def("conv2d", &conv2d);

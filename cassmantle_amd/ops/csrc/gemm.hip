@@ -34,6 +34,7 @@ bool buf_ok(const GemmArgs& p) {
     const char* e = getenv("CASSMANTLE_GEMM_BUF");
     force = e ? atoi(e) : 1;
   }
+  if (p.A2 != nullptr) return true;   // two-source A exists only on this path (host-checked sizes)
   if (!force || p.K % BK != 0) return false;
   const long long ldw = p.ldw ? p.ldw : p.K;
   const long long lim = (1LL << 31) - 1;

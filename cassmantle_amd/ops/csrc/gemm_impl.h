@@ -212,14 +212,15 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   // rocprof PMC).  Invalid rows / conv padding use voffset 0x80000000 >= num_records: the
   // buffer unit returns zeros (no zero page, no per-tile select).  Conv tap validity is a
   // per-lane bitmask over the ksize^2 taps.
-  __amdgpu_buffer_rsrc_t rsA, rsW;
+  __amdgpu_buffer_rsrc_t rsA, rsW, rsA2;
   int a_vo[BUF ? AR : 1], a_mask[BUF ? AR : 1], w_vo[BUF ? WR : 1];
+  int a_vo2[(BUF && CONV == 0) ? AR : 1];   // second A source (channel concatenation, p.A2)
   if constexpr (BUF) {
     constexpr int OOB = (int)0x80000000;
     long long biasA = 0;   // bytes: lowest pixel offset a conv tap can address is -bias
     if constexpr (CONV == 2) biasA = ((long long)p.pad * p.IW + p.pad) * p.Cin * 2;
     const long long a_bytes = CONV ? (long long)p.M / (p.Ho * p.Wo) * p.IH * p.IW * p.Cin * 2
-                                   : ((long long)(p.M - 1) * p.lda + p.K) * 2;
+                                   : ((long long)(p.M - 1) * p.lda + (p.A2 ? p.ka : p.K)) * 2;
     rsA = make_rsrc((const char*)A - biasA, a_bytes + biasA);
     const long long w_bytes = ((long long)(p.Nw - 1) * ldw + p.K) * 2;
     rsW = make_rsrc(W, w_bytes);
@@ -241,6 +242,16 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) w_vo[i] = w_row[i] >= 0 ? (int)(w_off[i] * 2) : OOB;
+    if constexpr (CONV == 0) {
+      if (p.A2 != nullptr) {   // k >= ka: rows of A2 (row stride lda2), k offset k0 - ka
+        rsA2 = make_rsrc(p.A2, ((long long)(p.M - 1) * p.lda2 + (p.K - p.ka)) * 2);
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const int r = RR * i + rsub;
+          a_vo2[i] = a_ok[i] ? (int)(((long long)(m0 + r) * p.lda2 + a_chunk[i] * 8) * 2) : OOB;
+        }
+      }
+    }
   }
 
   // wave-uniform conv tap state for CONV >= 2 (Cin % 64 == 0: a k-tile is 64 channels of one
@@ -272,11 +283,21 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         soffA = ((t_ky * p.IW + t_kx) * p.Cin + t_ci) * 2;
         tap = t_ky * p.ksize + t_kx;
       }
+      if constexpr (CONV == 0) {
+        if (p.A2 != nullptr && k0 >= p.ka) {        // wave-uniform: this k-tile lies in A2
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        int vo = a_vo[i];
-        if constexpr (CONV == 2) vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
-        blds16(rsA, As + (RR * i + 8 * wave) * 8, vo, soffA);
+          for (int i = 0; i < AR; ++i) blds16(rsA2, As + (RR * i + 8 * wave) * 8, a_vo2[i], (k0 - p.ka) * 2);
+        } else {
+#pragma unroll
+          for (int i = 0; i < AR; ++i) blds16(rsA, As + (RR * i + 8 * wave) * 8, a_vo[i], soffA);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          int vo = a_vo[i];
+          if constexpr (CONV == 2) vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
+          blds16(rsA, As + (RR * i + 8 * wave) * 8, vo, soffA);
+        }
       }
 #pragma unroll
       for (int i = 0; i < WR; ++i) {
@@ -598,18 +619,22 @@ __global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ parti
   }
 }
 
-// split-K reduce + GroupNorm statistics of the output (p.stats): block = 64 column quads x 4
-// row lanes over RB rows; each thread sums the slabs of its quad for RB/4 rows, runs the
-// epilogue, and accumulates (sum, sumsq) of the stored bf16 values; the 4 row lanes are folded
-// in LDS and added with one atomic per (column, statistic) per block (per-thread flushes when a
-// block's rows straddle images)
-constexpr int SK_RB = 32;
+// split-K reduce + GroupNorm statistics of the output (p.stats): block = 16 column quads (64
+// columns) x 16 row lanes over SK_RB = 64 rows; each thread sums the slabs of its quad for 4 rows
+// (4 slab loads in flight), runs the epilogue and accumulates (sum, sumsq) of the stored bf16
+// values; the 16 row lanes are folded in LDS and added with one atomic per (column, statistic)
+// per block (per-thread flushes when a block's rows straddle images).  The fp32 atomics, not the
+// slab reads, bound this pass when blocks are small: 4 row lanes x 16 rows cost +9 us on the
+// 16x16-level conv (327k atomics), 16 x 64 is ~4x fewer.
+constexpr int SK_RB = 64;
+constexpr int SK_QB = 16;                  // column quads per block
+constexpr int SK_RL = 256 / SK_QB;         // row lanes
 template <bool OUTF32>
 __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, const float* __restrict__ partial,
                                                                   int split) {
-  __shared__ float red[2][4][256];
-  const int qd = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int n = (blockIdx.x * 64 + qd) * 4;
+  __shared__ float red[2][SK_RL][SK_QB * 4];
+  const int qd = threadIdx.x % SK_QB, rl = threadIdx.x / SK_QB;
+  const int n = (blockIdx.x * SK_QB + qd) * 4;
   const int m0 = blockIdx.y * SK_RB;
   const int m1 = min(p.M, m0 + SK_RB);
   const bool on = n < p.N;
@@ -628,10 +653,23 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
     }
   };
   if (on) {
-    for (int m = m0 + rl; m < m1; m += 4) {
+    for (int m = m0 + rl; m < m1; m += SK_RL) {
       float o[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int sl = 0; sl < split; ++sl) {
-        const float4 v = *reinterpret_cast<const float4*>(partial + ((long long)sl * p.M + m) * p.N + n);
+      const float* src = partial + (long long)m * p.N + n;
+      const long long slab = (long long)p.M * p.N;
+      int sl = 0;
+      for (; sl + 4 <= split; sl += 4) {     // 4 slab loads in flight per thread
+        const float4 v0 = *reinterpret_cast<const float4*>(src + (sl + 0) * slab);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + (sl + 1) * slab);
+        const float4 v2 = *reinterpret_cast<const float4*>(src + (sl + 2) * slab);
+        const float4 v3 = *reinterpret_cast<const float4*>(src + (sl + 3) * slab);
+        o[0] += (v0.x + v1.x) + (v2.x + v3.x);
+        o[1] += (v0.y + v1.y) + (v2.y + v3.y);
+        o[2] += (v0.z + v1.z) + (v2.z + v3.z);
+        o[3] += (v0.w + v1.w) + (v2.w + v3.w);
+      }
+      for (; sl < split; ++sl) {
+        const float4 v = *reinterpret_cast<const float4*>(src + sl * slab);
         o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
       }
       epilogue4<OUTF32>(p, 0, m, n, o);      // (N % 8 == 0: o holds the final values)
@@ -658,12 +696,15 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
   }
   __syncthreads();
   const int img = m0 / shw;
-  for (int c = threadIdx.x; c < 512; c += 256) {
-    const int st = c >> 8, col = c & 255;
-    const int nn = blockIdx.x * 256 + col;
-    if (nn >= p.N) continue;
-    const float a = red[st][0][col] + red[st][1][col] + red[st][2][col] + red[st][3][col];
-    atomicAdd(p.stats + ((long long)img * p.N + nn) * 2 + st, a);
+  if (threadIdx.x < 2 * SK_QB * 4) {
+    const int st = threadIdx.x / (SK_QB * 4), col = threadIdx.x % (SK_QB * 4);
+    const int nn = blockIdx.x * SK_QB * 4 + col;
+    if (nn < p.N) {
+      float a = 0.f;
+#pragma unroll
+      for (int r = 0; r < SK_RL; ++r) a += red[st][r][col];
+      atomicAdd(p.stats + ((long long)img * p.N + nn) * 2 + st, a);
+    }
   }
 }
 
@@ -699,7 +740,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   }
   hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * WN), lds, s, p, ws);
   if (split > 1 && p.stats != nullptr) {
-    dim3 g2((unsigned)((p.N / 4 + 63) / 64), (unsigned)((p.M + SK_RB - 1) / SK_RB));
+    dim3 g2((unsigned)((p.N / 4 + SK_QB - 1) / SK_QB), (unsigned)((p.M + SK_RB - 1) / SK_RB));
     hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split);
   } else if (split > 1) {
     const long long nq = (long long)p.M * (p.N / 4);

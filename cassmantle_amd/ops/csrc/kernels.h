@@ -26,6 +26,10 @@ struct GemmArgs {
   // fused RMSNorm of A's rows (GEMV path only): A <- A * gamma / rms(A)
   const uint16_t* rms_gamma = nullptr;
   float rms_eps = 0.f;
+  // second A source (1x1 conv / linear over a channel concatenation [A | A2]): k < ka reads A
+  // (row stride lda), k >= ka reads A2 (row stride lda2); ka % 64 == 0 (whole k-tiles)
+  const uint16_t* A2 = nullptr;
+  int lda2 = 0, ka = 0;
   // GroupNorm statistics of the output: atomically accumulated per-(image, column) sum and
   // sum-of-squares [M / stats_hw][N][2] fp32 (zeroed by the caller); stats_hw = rows per image
   float* stats = nullptr;
@@ -61,8 +65,10 @@ void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s)
 void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        float* ws, int B, long long S, int C, int G, float eps, int silu, hipStream_t s);
 // GroupNorm from producer-accumulated per-channel stats ([B][Ca][2] for channels < Ca, then
-// [B][C-Ca][2] from stats_b when the input is a channel concatenation); no statistics pass
-void launch_group_norm_cs(const uint16_t* x, const float* stats_a, int Ca, const float* stats_b,
+// [B][C-Ca][2] from stats_b when the input is a channel concatenation); no statistics pass.
+// x2 != null: the input is the concatenation [x (Ca channels) | x2 (C - Ca channels)] read from
+// the two tensors (the concatenated tensor is never materialised)
+void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* stats_a, int Ca, const float* stats_b,
                           const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
                           int G, float eps, int silu, hipStream_t s);
 // per-channel stats of an NHWC tensor into zeroed [B][C][2] (for producers without a fused path)

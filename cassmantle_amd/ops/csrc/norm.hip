@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __
 // (UNet up-block skips) reads channels >= Ca from the second producer's statistics.
 template <int VPT>
 __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t* __restrict__ x,
+                                                                 const uint16_t* __restrict__ x2,
                                                                  const float* __restrict__ sa, int Ca,
                                                                  const float* __restrict__ sb,
                                                                  const uint16_t* __restrict__ gamma,
@@ -267,9 +268,26 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
   }
   const long long rbeg = (long long)blockIdx.x * rows_per_block;
   const long long rend = min(S, rbeg + rows_per_block);
-  const long long off = (long long)b * S * C;
-  const uint16_t* xb = x + off;
-  uint16_t* yb = y + off;
+  uint16_t* yb = y + (long long)b * S * C;
+  // source of each of this thread's 8-channel vectors: the input itself, or for a channel
+  // concatenation [x | x2] (UNet up-block skips, never materialised) x rows of Ca channels and
+  // x2 rows of C - Ca channels (Ca % 8 == 0: a vector never straddles the two)
+  const uint16_t* src[VPT];
+  int lds_[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int c0 = (tv + T * j) * 8;
+    if (x2 == nullptr) {
+      src[j] = x + (long long)b * S * C + c0;
+      lds_[j] = C;
+    } else if (c0 < Ca) {
+      src[j] = x + (long long)b * S * Ca + c0;
+      lds_[j] = Ca;
+    } else {
+      src[j] = x2 + (long long)b * S * Cb + (c0 - Ca);
+      lds_[j] = Cb;
+    }
+  }
   auto emit = [&](long long r, int j, uint4 u) {
     float f[8];
     unpack8(u, f);
@@ -288,7 +306,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
 #pragma unroll
       for (int j = 0; j < VPT; ++j) {
         const int v = tv + T * j;
-        if (v < V) u[k][j] = *reinterpret_cast<const uint4*>(xb + (r + (long long)k * R) * C + v * 8);
+        if (v < V) u[k][j] = *reinterpret_cast<const uint4*>(src[j] + (r + (long long)k * R) * lds_[j]);
       }
 #pragma unroll
     for (int k = 0; k < GN_UNROLL; ++k)
@@ -299,7 +317,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
   for (; r < rend; r += R)
 #pragma unroll
     for (int j = 0; j < VPT; ++j)
-      if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(xb + r * C + (tv + T * j) * 8));
+      if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(src[j] + r * lds_[j]));
 }
 
 // per-channel sum / sum-of-squares of an NHWC tensor, atomically added into [B][C][2]
@@ -454,7 +472,7 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        C, G, g.T, g.R, rpb, silu);
 }
 
-void launch_group_norm_cs(const uint16_t* x, const float* stats_a, int Ca, const float* stats_b,
+void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* stats_a, int Ca, const float* stats_b,
                           const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
                           int G, float eps, int silu, hipStream_t s) {
   const GnGeom g = gn_geom(C);
@@ -467,10 +485,10 @@ void launch_group_norm_cs(const uint16_t* x, const float* stats_a, int Ca, const
   const size_t shs = sizeof(float) * 2 * (G + C);
   if (stats_b == nullptr) Ca = C;
   if (g.VPT == 1)
-    hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, stats_a, Ca,
+    hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
                        stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
   else
-    hipLaunchKernelGGL(gn_apply_cs_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, stats_a, Ca,
+    hipLaunchKernelGGL(gn_apply_cs_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
                        stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
 }
 

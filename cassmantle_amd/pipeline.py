@@ -73,6 +73,16 @@ class _StepState:
             self.added = {k: torch.zeros_like(v) for k, v in added.items()}
         self.graph: Optional["torch.cuda.CUDAGraph"] = None
         self.plan = plan
+        # per-plan time conditioning (UNet.time_table), refilled in place every generation
+        self.temb_tab: Optional[torch.Tensor] = None
+        self.tb_tab: Optional[torch.Tensor] = None
+
+    def load_time(self, temb: torch.Tensor, tb: torch.Tensor) -> None:
+        if self.temb_tab is None:
+            self.temb_tab, self.tb_tab = temb.clone(), tb.clone()
+        else:
+            self.temb_tab.copy_(temb)
+            self.tb_tab.copy_(tb)
 
     def load(self, x0: torch.Tensor, ctx: torch.Tensor, added: Optional[dict]):
         self.x.copy_(x0)
@@ -134,9 +144,10 @@ class StableDiffusion:
 
     # ------------------------------------------------------------------ denoise
     def _unet_step(self, st: _StepState) -> None:
-        nb = st.unet_in.shape[0]
-        t = st.tsteps.index_select(0, st.step.long()).expand(nb)
-        eps = self.unet(st.unet_in, t, st.ctx, st.added, fp8=self.fp8)
+        idx = st.step.long()
+        # this step's rows of the per-plan time table (device index: graph-capturable)
+        cond = (st.temb_tab.index_select(0, idx)[0], st.tb_tab.index_select(0, idx)[0])
+        eps = self.unet(st.unet_in, None, st.ctx, st.added, fp8=self.fp8, time_cond=cond)
         ops.latent_step(eps, st.x, st.hist, st.xs, st.coef, st.step, st.unet_in, st.cfg)
         ops.advance_step(st.step)
 
@@ -170,6 +181,9 @@ class StableDiffusion:
         # cross-attention K/V of the (loop-invariant) text context: one GEMM per generation,
         # written into per-shape buffers that the captured step graph reads
         self.unet.set_context(ctx)
+        # time embedding + every ResNet's time bias for all timesteps of the plan: one batched
+        # MLP + GEMM per generation (in place, so a captured step graph reads the new values)
+        st.load_time(*self.unet.time_table(st.tsteps, st.unet_in.shape[0], added))
         if self.use_graphs and st.graph is None:
             st.load(latents, ctx, added)
             self._capture(st)

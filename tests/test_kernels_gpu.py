@@ -164,6 +164,33 @@ def test_group_norm_statistics_of_a_concatenation():
     assert rel_err(out, ref.group_norm(x, 32, g, b, 1e-5, True)) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,Ca,Cb,N", [(8, 16, 1280, 640, 640), (2, 32, 640, 320, 320), (3, 8, 64, 192, 96),
+                                         (2, 5, 320, 320, 320)])
+def test_concat_free_gemm_and_group_norm(B, H, Ca, Cb, N):
+    """UNet up-block [h | skip] consumers read the two tensors directly: the 1x1 shortcut GEMM
+    stages k-tiles from both, the GroupNorm normalises both into one output."""
+    a = rnd(B, H, H, Ca, seed=60) + 0.3
+    s = rnd(B, H, H, Cb, seed=61) - 0.2
+    x = torch.cat([a, s], dim=-1)
+    w = rnd(N, Ca + Cb, scale=(Ca + Cb) ** -0.5, seed=62)
+    bias = rnd(N, scale=0.1, seed=63)
+    st = torch.zeros(B, N, 2, device=DEV)
+    out = ops.linear_cat(a, s, w, bias, stats=st)
+    exp = ref.linear(x, w, bias)
+    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
+    exp_st = torch.zeros_like(st)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(st, exp_st) < 1e-4
+    sa, sb = torch.zeros(B, Ca, 2, device=DEV), torch.zeros(B, Cb, 2, device=DEV)
+    ops.channel_stats(a, sa)
+    ops.channel_stats(s, sb)
+    g = rnd(Ca + Cb, seed=64) * 0.5 + 1
+    be = rnd(Ca + Cb, seed=65) * 0.1
+    G = 32 if (Ca + Cb) % 32 == 0 else 8
+    y = ops.group_norm_cat(a, s, G, g, be, 1e-5, True, stats=sa, stats2=sb)
+    assert rel_err(y, ref.group_norm(x, G, g, be, 1e-5, True)) < 1e-2
+
+
 @pytest.mark.parametrize("D,rows", [(320, 333), (384, 333), (768, 333), (1280, 333), (32, 333), (640, 1),
                                     (4096, 7), (136, 45)])
 def test_layer_norm(D, rows):

@@ -144,3 +144,28 @@ def test_minilm_embeddings_normalised():
     m = MiniLMEncoder(TINY_BERT, seed=0)
     e = m.embed(["lantern", "a glowing river"], "cpu", pad_to=16)
     assert torch.allclose(e.norm(dim=-1), torch.ones(2), atol=1e-4)
+
+
+def test_time_table_matches_per_step_time_embedding():
+    """The sampler's per-plan time table (one batched MLP + GEMM per generation) must give the
+    same UNet output as the per-step time embedding, for SD-1.5-style and SDXL-style (add-embeds)
+    conditioning."""
+    import torch
+    from dataclasses import replace
+    from cassmantle_amd.models.unet import TINY_UNET, UNet
+    for cfg in (TINY_UNET, replace(TINY_UNET, addition_embed=True, addition_time_embed_dim=8,
+                                   projection_class_embeddings_input_dim=32 + 6 * 8)):
+        m = UNet(cfg, seed=4)
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(2, 8, 8, 4, generator=g).to(torch.bfloat16)
+        ctx = torch.randn(2, 77, 32, generator=g).to(torch.bfloat16)
+        added = None
+        if cfg.addition_embed:
+            added = {"time_ids": torch.tensor([[16., 16, 0, 0, 16, 16]] * 2),
+                     "text_embeds": torch.randn(2, 32, generator=g).to(torch.bfloat16)}
+        ts = torch.tensor([999.0, 500.0, 1.0])
+        temb, tb = m.time_table(ts, 2, added)
+        for e in range(3):
+            ref = m(x, ts[e].expand(2), ctx, added)
+            out = m(x, None, ctx, added, time_cond=(temb[e], tb[e]))
+            assert torch.equal(out, ref)
