@@ -1,3 +1,8 @@
+"""A/B of the split-K UNet convs with and without fused GroupNorm output statistics (the
+statistics ride the split-K reduce pass; prints us per call for each shape).
+
+    python tools/ab_conv_stats.py
+"""
 import torch, sys, json
 sys.path.insert(0, '.')
 from cassmantle_amd import ops
