@@ -40,7 +40,8 @@ _GN_FUSE = os.environ.get("CASSMANTLE_GN_FUSE", "1") != "0"   # A/B knob (0: two
 
 
 class StatsArena:
-    """GroupNorm statistics produced by GEMM/conv epilogues: one zeroed fp32 slab per forward.
+    """GroupNorm statistics produced by GEMM/conv epilogues: one zeroed slab per forward (int64
+    fixed point, see ``ops.new_stats``).
 
     A producer (conv / linear called with ``stats=arena.take(...)``) accumulates the
     per-(image, channel) sum and sum-of-squares of its output in its epilogue; the GroupNorm
@@ -68,7 +69,7 @@ class StatsArena:
         self.buf = self._bufs.get(key)
         need = self._need.get(key, 0)
         if need and self.buf is None:
-            self.buf = self._bufs[key] = torch.empty(need, device=x.device, dtype=torch.float32)
+            self.buf = self._bufs[key] = torch.empty(need, device=x.device, dtype=torch.int64)
         if self.buf is not None:
             self.buf.zero_()
         self.device = x.device
@@ -83,7 +84,7 @@ class StatsArena:
             s = self.buf[self.off:end].view(B, C, 2)
         else:
             self._need[self.key] = max(self._need.get(self.key, 0), end)
-            s = torch.zeros((B, C, 2), device=self.device, dtype=torch.float32)
+            s = ops.new_stats(B, C, self.device)
         self.off = end
         return s
 
@@ -154,9 +155,13 @@ class SelfAttention(nn.Module):
         self.to_qkv = Linear(dim, 3 * dim, bias=qkv_bias, gen=gen, dtype=dtype)
         self.to_out = Linear(dim, dim, bias=out_bias, gen=gen, dtype=dtype)
 
-    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False):
-        B, N, C = x.shape
-        qkv = self.to_qkv(x).view(B, N, 3, self.heads, self.head_dim)
+    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False, qkv=None):
+        """``qkv``: the fused projection already computed (e.g. with a folded LayerNorm)."""
+        if qkv is None:
+            qkv = self.to_qkv(x)
+        B, N = qkv.shape[0], qkv.shape[1]
+        C = self.dim
+        qkv = qkv.view(B, N, 3, self.heads, self.head_dim)
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, kv_lens=kv_lens, fp8=fp8)
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
@@ -172,9 +177,13 @@ class CrossAttention(nn.Module):
 
     _kv = None   # view into the UNet's batched context-K/V buffer (set by UNet.set_context)
 
-    def forward(self, x, ctx, residual=None, fp8=False):
-        B, N, C = x.shape
-        q = self.to_q(x).view(B, N, self.heads, self.head_dim)
+    def forward(self, x, ctx, residual=None, fp8=False, q=None):
+        """``q``: the query projection already computed (e.g. with a folded LayerNorm)."""
+        if q is None:
+            q = self.to_q(x)
+        B, N = q.shape[0], q.shape[1]
+        C = self.dim
+        q = q.view(B, N, self.heads, self.head_dim)
         if self._kv is not None and self._kv.shape[0] == B:
             # the text context is constant over the denoise loop: K/V of every cross-attention
             # layer come from ONE GEMM per generation (strided views, no copies)

@@ -9,6 +9,7 @@ nearest-2× upsample fused into the following conv, skip concatenation on the ch
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -101,6 +102,12 @@ class ResnetBlock(nn.Module):
         return self.conv2(h, residual=sc, stats=s2), s2          # residual fused in epilogue
 
 
+# LayerNorm folded into the following projection GEMM (row-statistics pass + epilogue
+# correction).  Measured neutral on SD-1.5 (684 vs 681 ms/step, profiles/r1_bench_lnfold_ab.jsonl):
+# the read-only statistics pass costs about what the LayerNorm kernel did, so it is opt-in.
+_LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "0") == "1"
+
+
 class BasicTransformerBlock(nn.Module):
     def __init__(self, dim: int, heads: int, ctx_dim: int, gen, dtype):
         super().__init__()
@@ -111,7 +118,32 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = LayerNorm(dim, 1e-5, dtype)
         self.ff = GEGLUFeedForward(dim, 4, gen=gen, dtype=dtype)
 
+    _folds = None   # LayerNorm-folded projection weights (ops.ln_fold), built on first HIP use
+
+    def folds(self):
+        """(W*gamma, wsum, b + W.beta) of norm1->to_qkv, norm2->to_q, norm3->ff.proj_in.  Reset
+        by UNet.fuse_projections (call it again after loading weights)."""
+        if self._folds is None:
+            self._folds = (ops.ln_fold(self.norm1.weight, self.norm1.bias, self.attn1.to_qkv.weight,
+                                       self.attn1.to_qkv.bias),
+                           ops.ln_fold(self.norm2.weight, self.norm2.bias, self.attn2.to_q.weight,
+                                       self.attn2.to_q.bias),
+                           ops.ln_fold(self.norm3.weight, self.norm3.bias, self.ff.proj_in.weight,
+                                       self.ff.proj_in.bias))
+        return self._folds
+
     def forward(self, x, ctx, fp8=False):
+        if _LN_FOLD and x.device.type == "cuda" and ops.get_mode() == "hip":
+            # the three LayerNorms are folded into the projections that consume them: a
+            # read-only row-statistics pass each, no normalised activation in HBM
+            f = self.folds()
+            n1, n2, n3 = self.norm1, self.norm2, self.norm3
+            qkv = ops.ln_linear(x, n1.weight, n1.bias, n1.eps, self.attn1.to_qkv.weight, fold=f[0])
+            x = self.attn1(None, residual=x, fp8=fp8, qkv=qkv)
+            q = ops.ln_linear(x, n2.weight, n2.bias, n2.eps, self.attn2.to_q.weight, fold=f[1])
+            x = self.attn2(None, ctx, residual=x, fp8=fp8, q=q)
+            h = ops.ln_linear(x, n3.weight, n3.bias, n3.eps, self.ff.proj_in.weight, act="geglu", fold=f[2])
+            return self.ff.proj_out(h, residual=x)
         x = self.attn1(self.norm1(x), residual=x, fp8=fp8)
         x = self.attn2(self.norm2(x), ctx, residual=x, fp8=fp8)
         x = self.ff(self.norm3(x), residual=x)
@@ -237,6 +269,9 @@ class UNet(nn.Module):
         (22 launch-bound M=B GEMMs per step -> 1) and every cross-attention's context K/V
         projection into ONE [sum 2C, D_ctx] GEMM (run once per generation by
         :meth:`set_context`).  Call again after loading weights."""
+        for blk in self.modules():
+            if isinstance(blk, BasicTransformerBlock):
+                blk._folds = None                                   # re-fold LayerNorms lazily
         rs = self.resnets()
         off = 0
         for r in rs:

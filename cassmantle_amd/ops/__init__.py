@@ -49,12 +49,29 @@ _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "
 
 
 # ----------------------------------------------------------------------------- GEMM (K6)
+# GroupNorm statistics produced by GEMM/conv epilogues are int64 FIXED POINT (ops/csrc/common.h):
+# sum x 2^24 and sum of squares x 2^16 per (image, channel).  Integer atomics are exact and
+# order-independent, so the fused path is bit-deterministic run to run.
+STAT_SCALE = (2.0 ** 24, 2.0 ** 16)
+
+
+def new_stats(B: int, C: int, device) -> torch.Tensor:
+    """A zeroed statistics buffer for ``stats=`` arguments: int64 [B, C, 2]."""
+    return torch.zeros((B, C, 2), device=device, dtype=torch.int64)
+
+
+def stats_to_float(stats: torch.Tensor) -> torch.Tensor:
+    """Decode fixed-point statistics -> float64 [..., 2] (sum, sum of squares)."""
+    sc = torch.tensor([1.0 / STAT_SCALE[0], 1.0 / STAT_SCALE[1]], dtype=torch.float64, device=stats.device)
+    return stats.double() * sc
+
+
 def channel_stats_ref(y: torch.Tensor, stats: torch.Tensor) -> None:
     """stats[b, c] += (sum, sum of squares) of y[b, ..., c] (the fused-epilogue contract)."""
     B, C = y.shape[0], y.shape[-1]
-    yf = y.reshape(B, -1, C).float()
-    stats[..., 0] += yf.sum(1)
-    stats[..., 1] += (yf * yf).sum(1)
+    yf = y.reshape(B, -1, C).double()
+    stats[..., 0] += torch.round(yf.sum(1) * STAT_SCALE[0]).to(torch.int64)
+    stats[..., 1] += torch.round((yf * yf).sum(1) * STAT_SCALE[1]).to(torch.int64)
 
 
 def channel_stats(y: torch.Tensor, stats: torch.Tensor) -> None:
@@ -70,7 +87,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu).
 
-    ``stats`` (fp32 [B, N, 2], zeroed; B = x.shape[0]): per-(image, channel) sum and
+    ``stats`` (:func:`new_stats` [B, N, 2], zeroed; B = x.shape[0]): per-(image, channel) sum and
     sum-of-squares of y are accumulated into it by the GEMM epilogue, for a following
     :func:`group_norm` (no statistics pass over y)."""
     if not _use_hip(x):
@@ -90,6 +107,57 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     r2 = residual.reshape(-1, N) if residual is not None else None
     hw = x2.shape[0] // x.shape[0] if stats is not None else 0
     ext().gemm(x2, w, bias, r2, out, _ACT[act], stats, hw)
+    return out.reshape(*x.shape[:-1], N)
+
+
+def ln_fold(ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], w: torch.Tensor,
+            bias: Optional[torch.Tensor] = None):
+    """Fold a LayerNorm's affine into the following linear layer:
+    LN(x) @ W^T + b = rstd * (x @ (W*gamma)^T - mean * wsum) + (b + W @ beta), so the GEMM can run
+    on the raw rows.  Returns (W*gamma [bf16], wsum = row sums of the bf16 W*gamma [fp32],
+    b + W @ beta [bf16]).  Recompute after loading weights."""
+    wf = (w.float() * ln_weight.float()[None, :]).to(w.dtype).contiguous()
+    wsum = wf.float().sum(1).contiguous()
+    b = torch.zeros(w.shape[0], device=w.device, dtype=torch.float32)
+    if ln_bias is not None:
+        b = b + w.float() @ ln_bias.float()
+    if bias is not None:
+        b = b + bias.float()
+    return wf, wsum, b.to(w.dtype).contiguous()
+
+
+def row_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """Per-row LayerNorm statistics (mean, rstd) of x [..., D] -> fp32 [rows, 2]."""
+    if not _use_hip(x):
+        xf = x.float().reshape(-1, x.shape[-1])
+        mean = xf.mean(-1)
+        var = xf.var(-1, unbiased=False)
+        return torch.stack([mean, (var + eps).rsqrt()], dim=-1)
+    out = torch.empty((x.numel() // x.shape[-1], 2), device=x.device, dtype=torch.float32)
+    ext().row_stats(x.contiguous(), out, float(eps))
+    return out
+
+
+def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], eps: float,
+              w: torch.Tensor, bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+              act: Optional[str] = None, fold=None) -> torch.Tensor:
+    """``linear(layer_norm(x), w, bias, residual, act)``.  With ``fold`` (:func:`ln_fold` of these
+    weights) on the HIP path the LayerNorm is folded into the GEMM: a read-only row-statistics
+    pass, then the GEMM on the raw rows with the folded weights and a per-row epilogue
+    correction — the normalised activation is never written or re-read."""
+    K = x.shape[-1]
+    rows = x.numel() // K
+    if fold is None or not _use_hip(x) or rows <= 8 or K % 8:
+        return linear(layer_norm(x, ln_weight, ln_bias, eps), w, bias, residual=residual, act=act)
+    wf, wsum, bf = fold
+    st = row_stats(x, eps)
+    x2 = x.reshape(rows, K)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    N = wf.shape[0] // 2 if act in ("geglu", "swiglu") else wf.shape[0]
+    out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
+    r2 = residual.reshape(rows, N) if residual is not None else None
+    ext().gemm(x2, wf, bf, r2, out, _ACT[act], None, 0, st, wsum)
     return out.reshape(*x.shape[:-1], N)
 
 
@@ -184,7 +252,7 @@ def _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias):
 def _group_norm_from_stats_ref(x, num_groups, weight, bias, eps, silu, stats):
     B, C = x.shape[0], x.shape[-1]
     S = x.numel() // (B * C)
-    st = stats.double().view(B, num_groups, C // num_groups, 2).sum(2)     # [B, G, 2]
+    st = stats_to_float(stats).view(B, num_groups, C // num_groups, 2).sum(2)     # [B, G, 2]
     n = S * (C // num_groups)
     mean = st[..., 0] / n
     var = (st[..., 1] / n - mean * mean).clamp_min(0)
@@ -202,7 +270,7 @@ def _group_norm_from_stats_ref(x, num_groups, weight, bias, eps, silu, stats):
 def group_norm(x: torch.Tensor, num_groups: int, weight: torch.Tensor, bias: torch.Tensor,
                eps: float, silu: bool = False, stats: Optional[torch.Tensor] = None,
                stats2: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """GroupNorm(+SiLU) over NHWC channels.  With ``stats`` (fp32 [B, C, 2] accumulated by the
+    """GroupNorm(+SiLU) over NHWC channels.  With ``stats`` (int64 [B, C, 2] accumulated by the
     producing GEMM/conv; for a channel concatenation ``stats`` covers the first channels and
     ``stats2`` the rest) the kernel skips its statistics pass."""
     if stats is not None:

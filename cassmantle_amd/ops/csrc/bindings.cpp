@@ -27,13 +27,13 @@ const uint16_t* opt_bptr(const c10::optional<at::Tensor>& t) {
 
 // plans split-K and allocates its fp32 partial slabs from the caching allocator (graph-pool
 // safe inside a capture), then launches on the current stream
-float* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N) {
+long long* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N) {
   if (!t.has_value() || !t->defined()) return nullptr;
   CHECK_DEV(*t);
   CHECK_CONTIG(*t);
-  TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == images * N * 2,
-              "stats must be a zeroed fp32 [images, N, 2] tensor");
-  return t->data_ptr<float>();
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() == images * N * 2,
+              "stats must be a zeroed int64 fixed-point [images, N, 2] tensor (ops.new_stats)");
+  return reinterpret_cast<long long*>(t->data_ptr<int64_t>());
 }
 
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
@@ -45,7 +45,7 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
   const GemmPlan plan = gemm_plan(p);
   p.cfg = plan.cfg;
   p.split = plan.split;
-  float* post_stats = nullptr;
+  long long* post_stats = nullptr;
   if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || p.batch != 1 || p.act == 4 || p.act == 6)) {
     post_stats = p.stats;
     p.stats = nullptr;
@@ -63,7 +63,8 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
 
 void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act,
-          const c10::optional<at::Tensor>& stats, int64_t stats_hw) {
+          const c10::optional<at::Tensor>& stats, int64_t stats_hw,
+          const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
@@ -90,7 +91,27 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     p.stats_hw = (int)stats_hw;
     p.stats = opt_stats(stats, p.M / stats_hw, p.N);
   }
+  if (ln_rows.has_value() && ln_rows->defined()) {
+    // folded LayerNorm: raw rows in, per-row (mean, rstd) + column sums of the folded weights
+    TORCH_CHECK(ln_wsum.has_value() && ln_wsum->defined(), "gemm: ln_rows needs ln_wsum");
+    CHECK_DEV(*ln_rows); CHECK_CONTIG(*ln_rows); CHECK_DEV(*ln_wsum); CHECK_CONTIG(*ln_wsum);
+    TORCH_CHECK(ln_rows->scalar_type() == at::kFloat && ln_rows->numel() == 2LL * p.M, "gemm: ln_rows fp32 [M, 2]");
+    TORCH_CHECK(ln_wsum->scalar_type() == at::kFloat && ln_wsum->numel() == p.Nw, "gemm: ln_wsum fp32 [Nw]");
+    TORCH_CHECK(p.M > 8 && p.K % 8 == 0 && p.lda % 8 == 0, "gemm: folded LayerNorm needs the MFMA path (M > 8)");
+    TORCH_CHECK(!p.out_f32 || p.act == 0, "gemm: folded LayerNorm with fp32 output supports no activation");
+    p.ln_rows = ln_rows->data_ptr<float>();
+    p.ln_wsum = ln_wsum->data_ptr<float>();
+  }
   run_gemm(p, out);
+}
+
+// per-row LayerNorm statistics (mean, rstd) of x [..., D] -> out fp32 [rows, 2]
+void row_stats(const at::Tensor& x, at::Tensor& out, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_CONTIG(out);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "row_stats: D % 8 == 0 and D <= 4096");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == 2 * (x.numel() / D), "row_stats: out fp32 [rows, 2]");
+  launch_row_stats(bptr(x), out.data_ptr<float>(), x.numel() / D, D, (float)eps, cur_stream());
 }
 
 // y = [x | x2] @ w^T + bias (+ residual, + output statistics) without materialising the channel
@@ -220,19 +241,19 @@ void group_norm_stats(const at::Tensor& x, const at::Tensor& stats_a, const c10:
   const int C = (int)x.size(-1);
   const long long S = x.numel() / ((long long)B * C);
   TORCH_CHECK(C % 8 == 0 && C % groups == 0, "group_norm_stats: C must be a multiple of 8 and of groups");
-  TORCH_CHECK(stats_a.scalar_type() == at::kFloat && stats_a.is_contiguous() && stats_a.dim() == 3 &&
-              stats_a.size(0) == B && stats_a.size(2) == 2, "group_norm_stats: stats_a must be fp32 [B, Ca, 2]");
+  TORCH_CHECK(stats_a.scalar_type() == at::kLong && stats_a.is_contiguous() && stats_a.dim() == 3 &&
+              stats_a.size(0) == B && stats_a.size(2) == 2, "group_norm_stats: stats_a must be int64 [B, Ca, 2]");
   const int Ca = (int)stats_a.size(1);
-  const float* sb = nullptr;
+  const long long* sb = nullptr;
   if (stats_b.has_value() && stats_b->defined()) {
-    TORCH_CHECK(stats_b->scalar_type() == at::kFloat && stats_b->is_contiguous() && stats_b->dim() == 3 &&
+    TORCH_CHECK(stats_b->scalar_type() == at::kLong && stats_b->is_contiguous() && stats_b->dim() == 3 &&
                 stats_b->size(0) == B && stats_b->size(1) == C - Ca && stats_b->size(2) == 2,
-                "group_norm_stats: stats_b must be fp32 [B, C - Ca, 2]");
-    sb = stats_b->data_ptr<float>();
+                "group_norm_stats: stats_b must be int64 [B, C - Ca, 2]");
+    sb = reinterpret_cast<const long long*>(stats_b->data_ptr<int64_t>());
   } else {
     TORCH_CHECK(Ca == C, "group_norm_stats: stats_a must cover every channel");
   }
-  launch_group_norm_cs(bptr(x), nullptr, stats_a.data_ptr<float>(), Ca, sb, bptr(gamma), bptr(beta), bptr_mut(out), B, S, C,
+  launch_group_norm_cs(bptr(x), nullptr, reinterpret_cast<const long long*>(stats_a.data_ptr<int64_t>()), Ca, sb, bptr(gamma), bptr(beta), bptr_mut(out), B, S, C,
                        (int)groups, (float)eps, (int)silu, cur_stream());
 }
 
@@ -250,10 +271,10 @@ void group_norm_cat(const at::Tensor& x, const at::Tensor& x2, const at::Tensor&
   TORCH_CHECK(x2.size(0) == B && x2.numel() == (long long)B * S * Cb && out.numel() == (long long)B * S * C &&
               out.size(-1) == C, "group_norm_cat: shapes must agree on batch and pixels");
   TORCH_CHECK(Ca % 8 == 0 && Cb % 8 == 0 && C % groups == 0, "group_norm_cat: channel counts");
-  TORCH_CHECK(stats_a.scalar_type() == at::kFloat && stats_a.is_contiguous() && stats_a.numel() == (long long)B * Ca * 2 &&
-              stats_b.scalar_type() == at::kFloat && stats_b.is_contiguous() && stats_b.numel() == (long long)B * Cb * 2,
-              "group_norm_cat: fp32 [B, C, 2] statistics of both inputs expected");
-  launch_group_norm_cs(bptr(x), bptr(x2), stats_a.data_ptr<float>(), Ca, stats_b.data_ptr<float>(), bptr(gamma),
+  TORCH_CHECK(stats_a.scalar_type() == at::kLong && stats_a.is_contiguous() && stats_a.numel() == (long long)B * Ca * 2 &&
+              stats_b.scalar_type() == at::kLong && stats_b.is_contiguous() && stats_b.numel() == (long long)B * Cb * 2,
+              "group_norm_cat: int64 [B, C, 2] statistics of both inputs expected");
+  launch_group_norm_cs(bptr(x), bptr(x2), reinterpret_cast<const long long*>(stats_a.data_ptr<int64_t>()), Ca, reinterpret_cast<const long long*>(stats_b.data_ptr<int64_t>()), bptr(gamma),
                        bptr(beta), bptr_mut(out), B, S, C, (int)groups, (float)eps, (int)silu, cur_stream());
 }
 
@@ -460,7 +481,10 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("out"),
+        py::arg("act"), py::arg("stats"), py::arg("stats_hw"), py::arg("ln_rows") = py::none(),
+        py::arg("ln_wsum") = py::none());
+  m.def("row_stats", &row_stats);
   m.def("gemm_cat", &gemm_cat);
   m.def("group_norm_cat", &group_norm_cat);
   m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });

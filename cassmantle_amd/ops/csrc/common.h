@@ -55,6 +55,20 @@ CM_DEVICE float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x));
 
 // activation codes shared with python (ops/__init__.py _ACT)
 // Gated acts (GEGLU: h*gelu(g), SWIGLU: h*silu(g)) read a [value; gate] weight of 2N rows.
+// GroupNorm statistics are accumulated as 64-bit FIXED-POINT integers (sum x 2^24, sum of squares
+// x 2^16): integer atomics are exact and order-independent, so the fused-statistics path is
+// bit-deterministic run to run (fp32 atomics made whole denoise runs differ at the bf16 level).
+// Range: |sum| < 5e11, sumsq < 1.4e14 per (image, channel); resolution 6e-8 / 1.5e-5.
+constexpr double STAT_SCALE_SUM = 16777216.0;
+constexpr double STAT_SCALE_SQ = 65536.0;
+CM_DEVICE void stat_atomic_add(long long* st, int which, float v) {
+  const double sc = which ? STAT_SCALE_SQ : STAT_SCALE_SUM;
+  atomicAdd(reinterpret_cast<unsigned long long*>(st), (unsigned long long)__double2ll_rn((double)v * sc));
+}
+CM_DEVICE double stat_decode(long long v, int which) {
+  return (double)v * (which ? (1.0 / STAT_SCALE_SQ) : (1.0 / STAT_SCALE_SUM));
+}
+
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_QUICK_GELU = 3, ACT_GEGLU = 4, ACT_GELU_TANH = 5,
            ACT_SWIGLU = 6 };
 

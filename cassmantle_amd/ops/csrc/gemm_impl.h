@@ -67,6 +67,13 @@ CM_DEVICE void add4(float* o, uint2 v) {
   o[0] += bf2f(v.x & 0xffff); o[1] += bf2f(v.x >> 16); o[2] += bf2f(v.y & 0xffff); o[3] += bf2f(v.y >> 16);
 }
 
+// folded LayerNorm (p.ln_rows): o = rstd_m * (acc - mean_m * wsum[n..n+3]) for the W rows n..n+3
+CM_DEVICE void ln_fold4(const GemmArgs& p, int m, int wn, float* o) {
+  const float2 ms = reinterpret_cast<const float2*>(p.ln_rows)[m];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, p.ln_wsum[wn + r], o[r]);
+}
+
 // epilogue for 4 consecutive output columns n..n+3 of row m (raw accumulators in o)
 template <bool OUTF32>
 CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
@@ -74,6 +81,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
   const long long cbs = p.ldcb ? p.ldcb : p.N;
   const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (cbs % 4 == 0);
+  if (p.ln_rows) ln_fold4(p, m, n, o);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
   if (full) {
@@ -443,10 +451,13 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
           for (int pi = 0; pi < TI / 2; ++pi) {
             const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;
             const int n = n0 + nl;
-            float o[4];
+            float o[4], hh[4], gg[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
+            if (p.ln_rows && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
+              float h = hh[r], g = gg[r];
               if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
               o[r] = gate_f(h, g, p.act);
             }
@@ -457,8 +468,10 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
           for (int i = 0; i < TI; ++i) {
             const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
             const int n = n0 + nl;
-            float o[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
-                          acc[i][j][3] * p.alpha};
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (p.ln_rows && n < p.N && m < p.M) ln_fold4(p, m, n, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
             if (n < p.N && m < p.M) {
               if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
               if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
@@ -517,8 +530,8 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         if (cur < 0) return;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, s8[e]);
-          atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, q8[e]);
+          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, 0, s8[e]);
+          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, 1, q8[e]);
           s8[e] = 0.f;
           q8[e] = 0.f;
         }
@@ -557,7 +570,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         if (n0 + col >= p.N) continue;
         float a = 0.f;
         for (int r = 0; r < RL; ++r) a += R[(stat * RL + r) * OBN + col];
-        atomicAdd(p.stats + ((long long)img0 * p.N + n0 + col) * 2 + stat, a);
+        stat_atomic_add(p.stats + ((long long)img0 * p.N + n0 + col) * 2 + stat, stat, a);
       }
       return;
     }
@@ -573,10 +586,13 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       for (int pi = 0; pi < TI / 2; ++pi) {
         const int n = n0 + wn * (BN / WN / 2) + 16 * pi + 4 * fq;
         if (n >= p.N) continue;
-        float o[4];
+        float o[4], hh[4], gg[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
+        if (p.ln_rows) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float h = acc[2 * pi][j][r], g = acc[2 * pi + 1][j][r];
+          float h = hh[r], g = gg[r];
           if (p.bias) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
           o[r] = gate_f(h, g, p.act);
         }
@@ -646,8 +662,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
     if (cur < 0) return;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, s4[e]);
-      atomicAdd(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, q4[e]);
+      stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, 0, s4[e]);
+      stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, 1, q4[e]);
       s4[e] = 0.f;
       q4[e] = 0.f;
     }
@@ -703,7 +719,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
       float a = 0.f;
 #pragma unroll
       for (int r = 0; r < SK_RL; ++r) a += red[st][r][col];
-      atomicAdd(p.stats + ((long long)img * p.N + nn) * 2 + st, a);
+      stat_atomic_add(p.stats + ((long long)img * p.N + nn) * 2 + st, st, a);
     }
   }
 }

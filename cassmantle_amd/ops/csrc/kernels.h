@@ -30,9 +30,15 @@ struct GemmArgs {
   // (row stride lda), k >= ka reads A2 (row stride lda2); ka % 64 == 0 (whole k-tiles)
   const uint16_t* A2 = nullptr;
   int lda2 = 0, ka = 0;
+  // LayerNorm folded into this GEMM (A = raw rows x, W = W * gamma, bias = bias + W . beta):
+  // out[m][n] = rstd[m] * (acc - mean[m] * wsum[n]) + bias[n] ...; ln_rows [M] (mean, rstd)
+  // float2, ln_wsum [Nw] fp32 column sums of the folded W
+  const float* ln_rows = nullptr;
+  const float* ln_wsum = nullptr;
   // GroupNorm statistics of the output: atomically accumulated per-(image, column) sum and
-  // sum-of-squares [M / stats_hw][N][2] fp32 (zeroed by the caller); stats_hw = rows per image
-  float* stats = nullptr;
+  // sum-of-squares [M / stats_hw][N][2] int64 fixed point (common.h; zeroed by the caller);
+  // stats_hw = rows per image
+  long long* stats = nullptr;
   int stats_hw = 0;
 };
 #define GEMM_MAX_SPLIT 16
@@ -68,14 +74,17 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
 // [B][C-Ca][2] from stats_b when the input is a channel concatenation); no statistics pass.
 // x2 != null: the input is the concatenation [x (Ca channels) | x2 (C - Ca channels)] read from
 // the two tensors (the concatenated tensor is never materialised)
-void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* stats_a, int Ca, const float* stats_b,
+void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long* stats_a, int Ca, const long long* stats_b,
                           const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
                           int G, float eps, int silu, hipStream_t s);
-// per-channel stats of an NHWC tensor into zeroed [B][C][2] (for producers without a fused path)
-void launch_channel_stats(const uint16_t* x, float* stats, int B, long long S, int C, hipStream_t s);
+// per-channel stats of an NHWC tensor into zeroed int64 fixed-point [B][C][2] (for producers
+// without a fused path)
+void launch_channel_stats(const uint16_t* x, long long* stats, int B, long long S, int C, hipStream_t s);
 long long group_norm_workspace(int B, long long S, int C);
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        long long rows, int D, float eps, hipStream_t s);
+// per-row (mean, rstd) float2 of [rows][D] (LayerNorm statistics for a folded-LN GEMM)
+void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s);
 void launch_rms_norm(const uint16_t* x, const uint16_t* gamma, uint16_t* y, long long rows, int D, float eps,
                      hipStream_t s);
 

@@ -213,8 +213,8 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __
 template <int VPT>
 __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ x2,
-                                                                 const float* __restrict__ sa, int Ca,
-                                                                 const float* __restrict__ sb,
+                                                                 const long long* __restrict__ sa, int Ca,
+                                                                 const long long* __restrict__ sb,
                                                                  const uint16_t* __restrict__ gamma,
                                                                  const uint16_t* __restrict__ beta,
                                                                  uint16_t* __restrict__ y, long long S, int C,
@@ -229,18 +229,20 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
   // channel (sum, sumsq) pairs -> LDS with one coalesced pass (all loads in flight at once: a
   // per-group serial walk of Cg dependent L2 loads cost ~Cg x 0.2 us in every block), then one
   // thread per group folds its Cg channels from LDS in fp64
-  float2* cst = reinterpret_cast<float2*>(gst + 2 * G);
-  for (int c = tid; c < C; c += GN_THREADS)
-    cst[c] = c < Ca ? *reinterpret_cast<const float2*>(sa + ((long long)b * Ca + c) * 2)
-                    : *reinterpret_cast<const float2*>(sb + ((long long)b * Cb + (c - Ca)) * 2);
+  long long* cst = reinterpret_cast<long long*>(gst + 2 * G);   // [C][2] int64 fixed point
+  for (int c = tid; c < C; c += GN_THREADS) {
+    const long long* src = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
+    cst[2 * c] = src[0];
+    cst[2 * c + 1] = src[1];
+  }
   __syncthreads();
   for (int g = tid; g < G; g += GN_THREADS) {
-    double s = 0.0, q = 0.0;
+    long long si = 0, qi = 0;            // exact integer fold of the group's channels
     for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      const float2 v = cst[c];
-      s += v.x;
-      q += v.y;
+      si += cst[2 * c];
+      qi += cst[2 * c + 1];
     }
+    const double s = stat_decode(si, 0), q = stat_decode(qi, 1);
     const double n = (double)S * Cg;
     const double mean = s / n;
     double var = q / n - mean * mean;
@@ -323,7 +325,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
 // per-channel sum / sum-of-squares of an NHWC tensor, atomically added into [B][C][2]
 template <int VPT>
 __global__ void __launch_bounds__(GN_THREADS) channel_stats_kernel(const uint16_t* __restrict__ x,
-                                                                   float* __restrict__ stats, long long S, int C,
+                                                                   long long* __restrict__ stats, long long S, int C,
                                                                    int T, int R, long long rows_per_chunk) {
   extern __shared__ float sh[];              // [2][R][C]
   const int V = C / 8;
@@ -365,12 +367,14 @@ __global__ void __launch_bounds__(GN_THREADS) channel_stats_kernel(const uint16_
     const int stat = c / C, ch = c - stat * C;
     float acc = 0.f;
     for (int k = 0; k < R; ++k) acc += sh[(long long)(stat * R + k) * C + ch];
-    atomicAdd(stats + ((long long)b * C + ch) * 2 + stat, acc);
+    stat_atomic_add(stats + ((long long)b * C + ch) * 2 + stat, stat, acc);
   }
 }
 
 // LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): T lanes per row, VPL vectors per lane
-template <int VPL, bool RMS>
+// STATS: write only the row (mean, rstd) as float2 into y (LayerNorm folded into the next GEMM,
+// whose epilogue applies them: no normalised copy of the activation is written or re-read)
+template <int VPL, bool RMS, bool STATS = false>
 __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gamma,
                           const uint16_t* __restrict__ beta, uint16_t* __restrict__ y,
                           long long rows, int D, int T, float eps) {
@@ -410,6 +414,10 @@ __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __rest
   for (int o = T >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float rstd = rsqrtf(ss / D + eps);
   if (!ok) return;
+  if constexpr (STATS) {
+    if (sl == 0) reinterpret_cast<float2*>(y)[row] = make_float2(mean, rstd);
+    return;
+  }
   uint4* yr = reinterpret_cast<uint4*>(y + row * D);
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
@@ -472,7 +480,7 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        C, G, g.T, g.R, rpb, silu);
 }
 
-void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* stats_a, int Ca, const float* stats_b,
+void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long* stats_a, int Ca, const long long* stats_b,
                           const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
                           int G, float eps, int silu, hipStream_t s) {
   const GnGeom g = gn_geom(C);
@@ -482,7 +490,7 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* st
     rpb = (long long)g.R * 2;
     nb = (S + rpb - 1) / rpb;
   }
-  const size_t shs = sizeof(float) * 2 * (G + C);
+  const size_t shs = sizeof(float) * 2 * G + sizeof(long long) * 2 * C;
   if (stats_b == nullptr) Ca = C;
   if (g.VPT == 1)
     hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
@@ -492,7 +500,7 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const float* st
                        stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
 }
 
-void launch_channel_stats(const uint16_t* x, float* stats, int B, long long S, int C, hipStream_t s) {
+void launch_channel_stats(const uint16_t* x, long long* stats, int B, long long S, int C, hipStream_t s) {
   const GnGeom g = gn_geom(C);
   const int chunks = gn_chunks(B, S, g.R);
   const long long rpc = (S + chunks - 1) / chunks;
@@ -505,15 +513,15 @@ void launch_channel_stats(const uint16_t* x, float* stats, int B, long long S, i
                        rpc);
 }
 
-template <int VPL, bool RMS>
+template <int VPL, bool RMS, bool STATS>
 static void launch_ln_t(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                         long long rows, int D, int T, float eps, hipStream_t s) {
   const long long rows_per_block = 4LL * (64 / T);
   dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block));
-  hipLaunchKernelGGL((ln_kernel<VPL, RMS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, T, eps);
+  hipLaunchKernelGGL((ln_kernel<VPL, RMS, STATS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, T, eps);
 }
 
-template <bool RMS>
+template <bool RMS, bool STATS = false>
 static void launch_ln(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                       long long rows, int D, float eps, hipStream_t s) {
   const int V = D / 8;
@@ -521,15 +529,19 @@ static void launch_ln(const uint16_t* x, const uint16_t* gamma, const uint16_t* 
   while (T < 64 && T * 8 < V) T <<= 1;                 // VPL <= 8 (D <= 4096)
   const int VPL = (V + T - 1) / T;
   switch (VPL) {
-    case 1: launch_ln_t<1, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 2: launch_ln_t<2, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 3: launch_ln_t<3, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 4: launch_ln_t<4, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 5: launch_ln_t<5, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 6: launch_ln_t<6, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 7: launch_ln_t<7, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    default: launch_ln_t<8, RMS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 1: launch_ln_t<1, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 2: launch_ln_t<2, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 3: launch_ln_t<3, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 4: launch_ln_t<4, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 5: launch_ln_t<5, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 6: launch_ln_t<6, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 7: launch_ln_t<7, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    default: launch_ln_t<8, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
   }
+}
+
+void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s) {
+  launch_ln<false, true>(x, nullptr, nullptr, reinterpret_cast<uint16_t*>(stats), rows, D, eps, s);
 }
 
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,

@@ -134,7 +134,7 @@ def test_epilogue_group_norm_statistics(kind, B, H, Cin, Cout):
     """GEMM/conv epilogue statistics (sum, sum of squares per image and channel) feeding the
     apply-only GroupNorm must equal the plain two-pass GroupNorm of the same tensor."""
     x = rnd(B, H, H, Cin, seed=50) + 0.25
-    st = torch.zeros(B, Cout, 2, device=DEV)
+    st = ops.new_stats(B, Cout, DEV)
     if kind == "conv":
         w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=51)
         y = ops.conv2d(x, w, rnd(Cout, scale=0.3, seed=52), stats=st)
@@ -143,7 +143,7 @@ def test_epilogue_group_norm_statistics(kind, B, H, Cin, Cout):
         y = ops.linear(x, w, rnd(Cout, scale=0.3, seed=52), residual=rnd(B, H, H, Cout, seed=53), stats=st)
     exp_st = torch.zeros_like(st)
     ops.channel_stats_ref(y, exp_st)
-    assert rel_err(st, exp_st) < 1e-4
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
     G = 32 if Cout % 32 == 0 else 4
     g = rnd(Cout, seed=54) * 0.5 + 1
     b = rnd(Cout, seed=55) * 0.1
@@ -154,7 +154,7 @@ def test_epilogue_group_norm_statistics(kind, B, H, Cin, Cout):
 def test_group_norm_statistics_of_a_concatenation():
     a = rnd(2, 16, 16, 640, seed=56) + 0.5
     s = rnd(2, 16, 16, 320, seed=57) - 0.25
-    sa, sb = torch.zeros(2, 640, 2, device=DEV), torch.zeros(2, 320, 2, device=DEV)
+    sa, sb = ops.new_stats(2, 640, DEV), ops.new_stats(2, 320, DEV)
     ops.channel_stats(a, sa)
     ops.channel_stats(s, sb)
     x = torch.cat([a, s], dim=-1)
@@ -174,14 +174,14 @@ def test_concat_free_gemm_and_group_norm(B, H, Ca, Cb, N):
     x = torch.cat([a, s], dim=-1)
     w = rnd(N, Ca + Cb, scale=(Ca + Cb) ** -0.5, seed=62)
     bias = rnd(N, scale=0.1, seed=63)
-    st = torch.zeros(B, N, 2, device=DEV)
+    st = ops.new_stats(B, N, DEV)
     out = ops.linear_cat(a, s, w, bias, stats=st)
     exp = ref.linear(x, w, bias)
     assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
     exp_st = torch.zeros_like(st)
     ops.channel_stats_ref(out, exp_st)
-    assert rel_err(st, exp_st) < 1e-4
-    sa, sb = torch.zeros(B, Ca, 2, device=DEV), torch.zeros(B, Cb, 2, device=DEV)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+    sa, sb = ops.new_stats(B, Ca, DEV), ops.new_stats(B, Cb, DEV)
     ops.channel_stats(a, sa)
     ops.channel_stats(s, sb)
     g = rnd(Ca + Cb, seed=64) * 0.5 + 1
@@ -189,6 +189,26 @@ def test_concat_free_gemm_and_group_norm(B, H, Ca, Cb, N):
     G = 32 if (Ca + Cb) % 32 == 0 else 8
     y = ops.group_norm_cat(a, s, G, g, be, 1e-5, True, stats=sa, stats2=sb)
     assert rel_err(y, ref.group_norm(x, G, g, be, 1e-5, True)) < 1e-2
+
+
+@pytest.mark.parametrize("rows,K,N,act,res", [(4096, 320, 960, None, False), (300, 640, 640, None, True),
+                                             (2048, 1280, 1280, "geglu", False), (64, 1280, 1280, None, False),
+                                             (4096, 320, 1280, "geglu", False)])
+def test_layer_norm_folded_into_gemm(rows, K, N, act, res):
+    """LN(x) @ W^T + b computed as rstd * (x @ (W*gamma)^T - mean * wsum) + (b + W.beta): row
+    statistics pass + GEMM epilogue correction, vs the explicit LayerNorm -> GEMM reference (also
+    through the split-K reduce pass for the 64-row shape)."""
+    x = rnd(rows, K, seed=70) * 1.5 + 0.3
+    g = rnd(K, seed=71) * 0.3 + 1
+    be = rnd(K, seed=72) * 0.2
+    Nw = 2 * N if act == "geglu" else N
+    w = rnd(Nw, K, scale=K ** -0.5, seed=73)
+    b = rnd(Nw, scale=0.1, seed=74)
+    r = rnd(rows, N, seed=75) if res else None
+    fold = ops.ln_fold(g, be, w, b)
+    out = ops.ln_linear(x, g, be, 1e-5, w, b, residual=r, act=act, fold=fold)
+    exp = ref.linear(ref.layer_norm(x, g, be, 1e-5), w, b, residual=r, act=act)
+    assert rel_err(out, exp) < 1.5e-2
 
 
 @pytest.mark.parametrize("D,rows", [(320, 333), (384, 333), (768, 333), (1280, 333), (32, 333), (640, 1),
