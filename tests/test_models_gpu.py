@@ -84,3 +84,18 @@ def test_sd15_end_to_end_one_image():
     sd = StableDiffusion(SPECS["sd15"], device="cuda", use_graphs=True)
     img = sd.generate_tensor(["A cubism style piece depicting the following: a lantern"], "blurry", [1], steps=4)
     assert img.shape == (1, 512, 512, 3) and img.dtype == torch.uint8
+
+
+def test_unet_is_bit_deterministic_run_to_run():
+    """The fused GroupNorm statistics use exact integer (fixed-point) atomics, so two evaluations
+    of the same inputs are bit-identical (fp32 atomics made them differ at the bf16 level)."""
+    from cassmantle_amd.models.unet import SD15_UNET, UNet
+    m = UNet(SD15_UNET, seed=1).cuda()
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(8, 32, 32, 4, generator=g).to(torch.bfloat16).cuda()
+    t = torch.full((8,), 700.0, device="cuda")
+    ctx = torch.randn(8, 77, 768, generator=g).to(torch.bfloat16).cuda()
+    with torch.no_grad():
+        a = m(x, t, ctx)
+        b = m(x, t, ctx)
+    assert torch.equal(a, b)
