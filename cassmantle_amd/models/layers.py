@@ -37,6 +37,7 @@ def _ones(shape, dtype) -> nn.Parameter:
 
 
 _GN_FUSE = os.environ.get("CASSMANTLE_GN_FUSE", "1") != "0"   # A/B knob (0: two-pass GroupNorm)
+_UP2 = os.environ.get("CASSMANTLE_UP2", "1") != "0"           # A/B knob (0: upsampled 3x3 conv)
 
 
 class StatsArena:
@@ -112,7 +113,24 @@ class Conv2d(nn.Module):
         self.weight = _param((cout, k, k, cin), 1.0 / math.sqrt(cin * k * k), gen, dtype)
         self.bias = _param((cout,), 0.02, gen, dtype) if bias else None
 
+    _w4 = None   # parity-folded 2x2 weights for the upsampling conv (ops.fold_upsample_weights)
+    _w4_key = None
+
+    def up2_weights(self):
+        """Folded per-parity weights of an upsampling 3x3 conv, refreshed when the weight
+        tensor changes (in-place loads bump its version counter)."""
+        key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
+        if self._w4 is None or self._w4_key != key:
+            self._w4 = ops.fold_upsample_weights(self.weight)
+            self._w4_key = key
+        return self._w4
+
     def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None):
+        if upsample and self.k == 3 and self.stride == 1 and _UP2 and x.device.type == "cuda" \
+                and ops.get_mode() == "hip" and self.cin % 64 == 0:
+            # nearest-2x upsample + 3x3 conv as four parity-class 2x2 convs (4/9 of the MACs)
+            return ops.conv2d_up2(x, self.weight, self.up2_weights(), self.bias, residual=residual,
+                                  chan_bias=chan_bias, stats=stats)
         if self.k == 1 and self.stride == 1 and not upsample and chan_bias is None:
             return ops.linear(x, self.weight.view(self.cout, self.cin), self.bias, residual=residual, stats=stats)
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, residual=residual,

@@ -232,6 +232,40 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
+# nearest-2x upsample + 3x3 conv (pad 1) == four 2x2 convs on the low-res input, one per output
+# parity (a, b): output row 2i+a reads input rows {i-1, i} (a = 0: taps W0 | W1+W2) or {i, i+1}
+# (a = 1: taps W0+W1 | W2); same along x.  4/9 of the MACs of the upsampled conv.
+_UP2_ROWS = ([[1.0, 0.0, 0.0], [0.0, 1.0, 1.0]], [[1.0, 1.0, 0.0], [0.0, 0.0, 1.0]])
+
+
+def fold_upsample_weights(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 3, 3, Cin] -> [4, Cout, 2, 2, Cin] per-parity 2x2 weights (fp32 sums, rounded once)."""
+    wf = w.float()
+    outs = []
+    for a in (0, 1):
+        ra = torch.tensor(_UP2_ROWS[a], device=w.device)
+        for b in (0, 1):
+            rb = torch.tensor(_UP2_ROWS[b], device=w.device)
+            outs.append(torch.einsum("tk,sl,oklc->otsc", ra, rb, wf))
+    return torch.stack(outs).to(w.dtype).contiguous()
+
+
+def conv2d_up2(x: torch.Tensor, w: torch.Tensor, w4: Optional[torch.Tensor] = None,
+               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+               chan_bias: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``conv2d(x, w, bias, padding=1, upsample=True, ...)`` for a 3x3 ``w``.  On the HIP path
+    (Cin % 64 == 0) it runs as four parity-class 2x2 convs (``w4`` = :func:`fold_upsample_weights`
+    of ``w``, folded on the fly if omitted) writing the interleaved 2H x 2W output."""
+    B, H, W, Cin = x.shape
+    if not _use_hip(x) or Cin % 64 or w.shape[1] != 3:
+        return conv2d(x, w, bias, 1, 1, residual=residual, upsample=True, chan_bias=chan_bias, stats=stats)
+    if w4 is None:
+        w4 = fold_upsample_weights(w)
+    out = torch.empty((B, 2 * H, 2 * W, w.shape[0]), device=x.device, dtype=x.dtype)
+    ext().conv2d_up2(x.contiguous(), w4, bias, residual, chan_bias, out, stats)
+    return out
+
+
 def _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias):
     import torch.nn.functional as F
     xi = x.permute(0, 3, 1, 2)

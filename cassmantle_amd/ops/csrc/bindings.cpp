@@ -46,7 +46,7 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
   p.cfg = plan.cfg;
   p.split = plan.split;
   long long* post_stats = nullptr;
-  if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || p.batch != 1 || p.act == 4 || p.act == 6)) {
+  if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || (p.batch != 1 && !p.parity) || p.act == 4 || p.act == 6)) {
     post_stats = p.stats;
     p.stats = nullptr;
   }
@@ -194,6 +194,46 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
     TORCH_CHECK(chan_bias->size(0) == x.size(0) && chan_bias->size(1) == p.N, "conv2d: chan_bias must be [B, Cout]");
   p.C = out.data_ptr();
   p.stats_hw = p.Ho * p.Wo;
+  p.stats = opt_stats(stats, x.size(0), p.N);
+  run_gemm(p, out);
+}
+
+// nearest-2x upsample + 3x3 conv (pad 1) as four 2x2 convs on the low-res input, one per output
+// parity class (4/9 of the MACs of the upsampled conv): w4 [4, Cout, 2, 2, Cin] are the folded
+// weights (ops.fold_upsample_weights), out [B, 2H, 2W, Cout]
+void conv2d_up2(const at::Tensor& x, const at::Tensor& w4, const c10::optional<at::Tensor>& bias,
+                const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& chan_bias, at::Tensor& out,
+                const c10::optional<at::Tensor>& stats) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w4); CHECK_CONTIG(w4); CHECK_CONTIG(out); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 4 && w4.dim() == 5 && w4.size(0) == 4 && w4.size(2) == 2 && w4.size(3) == 2 &&
+              w4.size(4) == x.size(3), "conv2d_up2: x [B,H,W,Cin], w4 [4,Cout,2,2,Cin]");
+  TORCH_CHECK(out.dim() == 4 && out.size(0) == x.size(0) && out.size(1) == 2 * x.size(1) &&
+              out.size(2) == 2 * x.size(2) && out.size(3) == w4.size(1), "conv2d_up2: out [B,2H,2W,Cout]");
+  GemmArgs p;
+  p.conv = 1;
+  p.parity = 1;
+  p.A = bptr(x); p.W = bptr(w4); p.bias = opt_bptr(bias); p.residual = opt_bptr(residual);
+  if (chan_bias.has_value() && chan_bias->defined()) {
+    CHECK_DEV(*chan_bias);
+    CHECK_BF16(*chan_bias);
+    TORCH_CHECK(chan_bias->dim() == 2 && chan_bias->stride(1) == 1 && chan_bias->size(0) == x.size(0) &&
+                chan_bias->size(1) == out.size(3), "conv2d_up2: chan_bias must be [B, Cout] rows");
+    p.chan_bias = bptr(*chan_bias);
+    p.ldcb = (int)chan_bias->stride(0);
+  }
+  p.IH = (int)x.size(1); p.IW = (int)x.size(2); p.Cin = (int)x.size(3);
+  p.ksize = 2; p.stride = 1; p.pad = 1; p.upsample = 0;
+  p.Ho = p.IH; p.Wo = p.IW;                       // GEMM rows: the low-res grid of each class
+  p.N = (int)out.size(3); p.Nw = p.N;
+  p.M = (int)(x.size(0) * p.Ho * p.Wo);
+  p.K = 4 * p.Cin;
+  p.lda = p.Cin; p.ldc = p.N;
+  p.batch = 4;                                    // grid z = parity class
+  p.sA = 0; p.sW = (long long)p.N * 4 * p.Cin; p.sC = 0;
+  TORCH_CHECK(p.Cin % 64 == 0, "conv2d_up2: Cin % 64 == 0 (buffer-DMA conv path)");
+  if (residual.has_value() && residual->defined()) TORCH_CHECK(residual->numel() == out.numel(), "conv2d_up2: residual shape");
+  p.C = out.data_ptr();
+  p.stats_hw = p.Ho * p.Wo;                       // per image: every class adds its quarter
   p.stats = opt_stats(stats, x.size(0), p.N);
   run_gemm(p, out);
 }
@@ -490,6 +530,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });
   m.def("gemm_rms", &gemm_rms);
   m.def("conv2d", &conv2d);
+  m.def("conv2d_up2", &conv2d_up2);
   m.def("bmm_nt", &bmm_nt);
   m.def("group_norm", &group_norm);
   m.def("layer_norm", &layer_norm);

@@ -74,6 +74,18 @@ CM_DEVICE void ln_fold4(const GemmArgs& p, int m, int wn, float* o) {
   for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, p.ln_wsum[wn + r], o[r]);
 }
 
+// output row of GEMM row m.  Parity-upsample mode (p.parity, nearest-2x upsample + 3x3 conv as
+// four 2x2 convs on the low-res input, one per output parity class z = 2a + b = blockIdx.z):
+// GEMM row m = (image, i, j) of the low-res grid writes output pixel (2i + a, 2j + b).
+CM_DEVICE long long out_row(const GemmArgs& p, int m, int z) {
+  if (!p.parity) return m;
+  const int hw = p.Ho * p.Wo;
+  const int img = m / hw;
+  const int r = m - img * hw;
+  const int i = r / p.Wo, j = r - i * p.Wo;
+  return ((long long)img * 2 * p.Ho + 2 * i + (z >> 1)) * (2 * p.Wo) + 2 * j + (z & 1);
+}
+
 // epilogue for 4 consecutive output columns n..n+3 of row m (raw accumulators in o)
 template <bool OUTF32>
 CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
@@ -81,6 +93,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   const int bimg = (p.chan_bias != nullptr) ? (m / hw) : 0;
   const long long cbs = p.ldcb ? p.ldcb : p.N;
   const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (cbs % 4 == 0);
+  const long long om = out_row(p, m, batch);
   if (p.ln_rows) ln_fold4(p, m, n, o);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
@@ -91,12 +104,12 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
     }
-    if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
+    if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + om * p.ldc + n));
     if constexpr (OUTF32) {
-      float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
+      float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + om * p.ldc + n;
       *reinterpret_cast<float4*>(C) = make_float4(o[0], o[1], o[2], o[3]);
     } else {
-      uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
+      uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + om * p.ldc + n;
       *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
     }
   } else {   // ragged N (3-channel conv_out): element-wise tail
@@ -107,11 +120,11 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
       if (p.bias) v += bf2f(p.bias[n + r]);
       if (p.chan_bias) v += bf2f(p.chan_bias[(long long)bimg * cbs + n + r]);
       v = apply_act(v, p.act);
-      if (p.residual) v += bf2f(p.residual[(long long)m * p.ldc + n + r]);
+      if (p.residual) v += bf2f(p.residual[om * p.ldc + n + r]);
       if constexpr (OUTF32)
-        reinterpret_cast<float*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = v;
+        reinterpret_cast<float*>(p.C)[(long long)batch * p.sC + om * p.ldc + n + r] = v;
       else
-        reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n + r] = f2bf(v);
+        reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + om * p.ldc + n + r] = f2bf(v);
     }
   }
 }
@@ -181,8 +194,11 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       const int rr = m - b * hw;
       const int oy = rr / p.Wo;
       const int ox = rr - oy * p.Wo;
-      cy_[i] = oy * p.stride - p.pad;
-      cx_[i] = ox * p.stride - p.pad;
+      // parity-upsample mode: 2x2 taps at offsets {a-1, a} x {b-1, b} (pad 1-a / 1-b)
+      const int pad_y = p.parity ? 1 - (batch >> 1) : p.pad;
+      const int pad_x = p.parity ? 1 - (batch & 1) : p.pad;
+      cy_[i] = oy * p.stride - pad_y;
+      cx_[i] = ox * p.stride - pad_x;
       cbh_[i] = b * p.IH;
       a_off[i] = (((long long)b * p.IH + cy_[i]) * p.IW + cx_[i]) * p.Cin + a_chunk[i] * 8;
       if (!a_ok[i]) cy_[i] = -(1 << 28);   // never in bounds
@@ -489,9 +505,10 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
       auto finish = [&](int row, int c8) -> uint4 {   // residual add + store of one 16-B chunk
         const int m = m0 + row, n = n0 + c8 * 8;
+        const long long om = out_row(p, m, batch);
         uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
         if (p.residual) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + (long long)m * p.ldc + n);
+          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + om * p.ldc + n);
           float a[8], b[8];
           unpack8(v, a);
           unpack8(rv, b);
@@ -499,7 +516,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
           for (int e = 0; e < 8; ++e) a[e] += b[e];
           v = pack8(a);
         }
-        *reinterpret_cast<uint4*>(Cb + (long long)m * p.ldc + n) = v;
+        *reinterpret_cast<uint4*>(Cb + om * p.ldc + n) = v;
         return v;
       };
       if (p.stats == nullptr) {

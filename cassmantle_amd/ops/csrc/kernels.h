@@ -23,6 +23,10 @@ struct GemmArgs {
   int cfg = 0;                         // tile config index (gemm_plan)
   // implicit-GEMM convolution (conv != 0)
   int conv = 0, IH = 0, IW = 0, Cin = 0, Ho = 0, Wo = 0, stride = 1, pad = 0, ksize = 1, upsample = 0;
+  // parity-upsample conv (nearest-2x upsample + 3x3 conv as four 2x2 convs on the low-res input,
+  // 4/9 of the MACs): grid z = parity class 2a+b, W = [4][Cout][2][2][Cin] folded weights
+  // (sW = one class), Ho/Wo = low-res size, output written at pixel (2i+a, 2j+b)
+  int parity = 0;
   // fused RMSNorm of A's rows (GEMV path only): A <- A * gamma / rms(A)
   const uint16_t* rms_gamma = nullptr;
   float rms_eps = 0.f;

@@ -89,6 +89,26 @@ def test_conv(B, H, W, Cin, Cout, stride, up):
     assert rel_err(out, exp) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 8, 8, 128, 64), (8, 16, 16, 1280, 1280), (1, 32, 32, 256, 256),
+                                          (2, 6, 10, 64, 96), (4, 64, 64, 512, 512)])
+def test_conv_upsample_as_parity_2x2_convs(B, H, W, Cin, Cout):
+    """nearest-2x upsample + 3x3 conv computed as four parity-class 2x2 convs on the low-res
+    input (folded weights, interleaved output) vs the upsampled 3x3 conv reference, with every
+    epilogue input (bias, per-image bias, residual, GroupNorm statistics)."""
+    x = rnd(B, H, W, Cin, seed=80)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=81)
+    b = rnd(Cout, scale=0.1, seed=82)
+    cb = rnd(B, Cout, scale=0.1, seed=83)
+    res = rnd(B, 2 * H, 2 * W, Cout, seed=84)
+    st = ops.new_stats(B, Cout, DEV)
+    out = ops.conv2d_up2(x, w, None, b, residual=res, chan_bias=cb, stats=st)
+    exp = ref.conv2d(x, w, b, 1, 1, res, True, cb)
+    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
+    exp_st = ops.new_stats(B, Cout, DEV)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+
+
 def test_conv_epilogue_fusions():
     B, H, W, C = 2, 16, 16, 64
     x = rnd(B, H, W, C, seed=15)
