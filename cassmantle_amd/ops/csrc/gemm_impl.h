@@ -399,11 +399,16 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       for (int i = 0; i < TI; ++i) wf[i] = as_bf16x8(Bs[w_rd[ks] + 16 * 8 * i]);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) af[j] = as_bf16x8(Bs[a_rd[ks] + 16 * 8 * j]);
+      // raised wave priority while issuing the MFMA cluster (guide T5): with 2 blocks per CU the
+      // wave that has MFMA work keeps the pipe busy while the other waits on its LDS-DMA
+      // (+1..13 % on the SD convs / GEMMs, profiles/r1_ops_setprio_ab.txt)
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
   };
 
