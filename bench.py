@@ -157,7 +157,7 @@ def main() -> int:
                                 + (", fp8 attention" if args.fp8_attention else ""),
                        "global_batch": world * args.batch, "seq_len": (spec.resolution // 8) ** 2,
                        "parallelism": f"dp{world} (rooms)"},
-            "ops": "torch-eager" if args.baseline else "hip",
+            "ops": ("torch-eager" if args.baseline else "hip") if device.type == "cuda" else "cpu-reference",
             "graphs": bool(sd.use_graphs),
             "finite": finite,
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
