@@ -22,8 +22,11 @@ constexpr int BK = 64;
 //   5: 256x160 (4x2, wave 64x80)   6: 256x128 (4x2, wave 64x64)
 struct TileCfg { int BM, BN; float eff; int slots; };
 constexpr int kNumTiles = 7;
+// slots = resident blocks on the chip: 128x64 needs 48 KiB of LDS per block, so 3 blocks fit a
+// CU (768 slots); with 512 the model undercounted it and missed the measured best on the
+// level-2..4 plain GEMMs (profiles/r1_gemm_plan_sweep.jsonl: 14.5 vs 17.8 us at 8192x640x640)
 constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f, 512}, {256, 64, 0.95f, 512},
-                                       {128, 64, 0.80f, 512},  {256, 16, 0.25f, 512},  {256, 160, 1.02f, 256},
+                                       {128, 64, 0.80f, 768},  {256, 16, 0.25f, 512},  {256, 160, 1.02f, 256},
                                        {256, 128, 1.00f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
