@@ -136,6 +136,11 @@ def main() -> int:
         score = {"p50_score_ms": float(np.percentile(lat, 50)), "p99_score_ms": float(np.percentile(lat, 99)),
                  "score_batch": len(pairs)}
 
+    from cassmantle_amd.utils.tracing import TRACER
+    TRACER.flush()
+    stage_ms = {k: v["mean_ms"] for k, v in TRACER.snapshot().items()
+                if k in ("encode", "denoise", "decode")}
+
     if rank == 0:
         images = world * args.batch * args.steps
         value = images / elapsed
@@ -161,6 +166,7 @@ def main() -> int:
             "graphs": bool(sd.use_graphs),
             "finite": finite,
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
+            "stage_mean_ms": stage_ms,      # device time per generation (incl. warmup)
             **score,
         }
         print(json.dumps(out), flush=True)

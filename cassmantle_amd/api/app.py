@@ -37,6 +37,7 @@ from fastapi.staticfiles import StaticFiles
 
 from ..config import Config
 from ..game.service import GameService
+from ..utils.tracing import TRACER
 from .ratelimit import RateLimiter
 
 log = logging.getLogger("cassmantle")
@@ -185,7 +186,7 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
 
     @app.get("/healthz")
     async def healthz():
-        return {"ok": True, **service.stats()}
+        return {"ok": True, **service.stats(), "stages": TRACER.snapshot()}
 
     @app.get("/metrics")
     async def metrics():
@@ -205,7 +206,7 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         ]
         for k, v in (st.get("score_latency") or {}).items():
             lines.append(f"cassmantle_score_latency_{k} {v}")
-        return PlainTextResponse("\n".join(lines) + "\n")
+        return PlainTextResponse("\n".join(lines) + "\n" + TRACER.render_prometheus())
 
     return app
 

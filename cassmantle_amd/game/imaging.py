@@ -19,6 +19,8 @@ from typing import Callable, Optional, Tuple
 import numpy as np
 from PIL import Image, ImageFilter
 
+from ..utils.tracing import TRACER
+
 
 def score_to_blur(score: float, min_blur: float = 0.0, max_blur: float = 15.0) -> float:
     return min_blur + (1.0 - score ** 2) * (max_blur - min_blur)
@@ -82,7 +84,8 @@ class BlurCache:
             if ver != version:
                 arr = decode_jpeg(jpeg)
                 self._decoded = (version, arr)
-        out = encode_jpeg(self.blur_fn(arr, r), self.quality) if r > 0 else jpeg
+        with TRACER.span("blur_jpeg"):
+            out = encode_jpeg(self.blur_fn(arr, r), self.quality) if r > 0 else jpeg
         with self._lock:
             self._lru[key] = out
             while len(self._lru) > self.capacity:

@@ -28,6 +28,7 @@ from .models.schedulers import SchedulePlan, make_plan
 from .models.text import CLIP_BIGG, CLIP_L, TINY_CLIP, CLIPTextEncoder, CLIPTextConfig
 from .models.unet import SD15_UNET, SDXL_UNET, TINY_UNET, UNet, UNetConfig
 from .models.vae import SD_VAE, SDXL_VAE, TINY_VAE, VAEConfig, VAEDecoder
+from .utils.tracing import span
 
 
 @dataclass
@@ -215,10 +216,14 @@ class StableDiffusion:
         with (torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()):
             if caller is not None:
                 self.stream.wait_stream(caller)     # inputs the caller produced
-            ctx, added = self.encode_prompt(prompts, negative)
-            x0 = self.init_latents(seeds, plan)
-            x = self.denoise(ctx, x0, plan, added)
-            img = self.vae.decode_uint8(x.to(self.dtype))
+            # per-stage device time (events on the generation stream: no host sync)
+            with span("encode", self.stream):
+                ctx, added = self.encode_prompt(prompts, negative)
+                x0 = self.init_latents(seeds, plan)
+            with span("denoise", self.stream):
+                x = self.denoise(ctx, x0, plan, added)
+            with span("decode", self.stream):
+                img = self.vae.decode_uint8(x.to(self.dtype))
         if caller is not None:
             caller.wait_stream(self.stream)
             img.record_stream(caller)

@@ -18,6 +18,7 @@ import numpy as np
 
 from ..game.room import Scorer
 from ..game.scoring import SimilarityBackend, score_pairs
+from ..utils.tracing import TRACER
 
 
 class DirectScorer(Scorer):
@@ -29,7 +30,9 @@ class DirectScorer(Scorer):
     async def score(self, pairs):
         t0 = time.perf_counter()
         out = score_pairs(self.backend, pairs, self.min_score)
-        self.latencies.append(time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        self.latencies.append(dt)
+        TRACER.observe("score_request", dt * 1e3)
         return out
 
     def embed_words(self, words):
@@ -69,7 +72,10 @@ class BatchingScorer(Scorer):
 
     def _run(self, flat):
         with self._lock:
-            return score_pairs(self.backend, flat, self.min_score)
+            t0 = time.perf_counter()
+            out = score_pairs(self.backend, flat, self.min_score)
+            TRACER.observe("score_batch", (time.perf_counter() - t0) * 1e3)
+            return out
 
     async def _flush(self):
         batch, self._queue = self._queue, []
@@ -92,6 +98,7 @@ class BatchingScorer(Scorer):
             if not fut.done():
                 fut.set_result(vals[off:off + n])
             self.latencies.append(now - t0)
+            TRACER.observe("score_request", (now - t0) * 1e3)
             off += n
 
     def latency_percentiles(self) -> dict:
