@@ -117,7 +117,8 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    finite = bool(torch.isfinite(img.float()).all().item())
+    # finiteness of the final LATENTS (the uint8 image is finite by construction)
+    finite = bool(sd.last_finite.item()) if sd.last_finite is not None else None
 
     score = {}
     if rank == 0 and not args.no_score:

@@ -63,7 +63,10 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     binding = os.path.join(CSRC, "bindings.cpp")
     inc, lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result", "-Wno-unused-variable"]
+    # -pragma-unroll-threshold: the GEMM epilogues fully unroll over up to 32 accumulator
+    # fragments; past the default limit the unroller gives up and the accumulators go to scratch
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result", "-Wno-unused-variable",
+              "-mllvm", "-pragma-unroll-threshold=100000"]
     cmds = []
     objs = []
     for src in hip_srcs:

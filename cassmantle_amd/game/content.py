@@ -12,6 +12,7 @@ prompt to the remote SDXL endpoint and returns ``PIL.Image``.  Implementations h
 from __future__ import annotations
 
 import hashlib
+import threading
 import time
 from typing import List, Optional, Sequence
 
@@ -57,3 +58,86 @@ class SolidImageGenerator(ImageGenerator):
                 raise ImageGenerationError("non-finite image")
             out.append(np.clip(img, 0, 255).astype(np.uint8))
         return out
+
+
+class _GenRequest:
+    __slots__ = ("prompts", "negative", "seeds", "done", "result", "error")
+
+    def __init__(self, prompts, negative, seeds) -> None:
+        self.prompts, self.negative, self.seeds = list(prompts), negative, list(seeds)
+        self.done = threading.Event()
+        self.result: Optional[List[np.ndarray]] = None
+        self.error: Optional[BaseException] = None
+
+
+class BatchingImageGenerator(ImageGenerator):
+    """Serialises and BATCHES the generation requests of several rooms that share one device
+    pipeline (single-GPU serving with ``num_rooms > 1``).
+
+    Each room calls :meth:`generate` from its own worker thread (``asyncio.to_thread``).  The
+    first caller to take the run lock becomes the leader: it waits ``window_s`` for concurrent
+    requests, concatenates up to ``max_batch`` images' worth of them (same negative prompt, FIFO)
+    into ONE ``inner.generate`` call (one UNet batch of 2 x images with CFG) and hands every
+    request its slice; the others wait on their event and lead the next batch if theirs was not
+    taken.  The reference's rooms would each POST to the remote endpoint
+    (``src/backend.py:270-295``); here concurrent rooms become one batched denoise loop, and the
+    device pipeline is never driven by two threads at once."""
+
+    def __init__(self, inner: ImageGenerator, max_batch: int = 4, window_s: float = 0.02) -> None:
+        self.inner = inner
+        self.resolution = getattr(inner, "resolution", 512)
+        self.max_batch = max(1, int(max_batch))
+        self.window_s = window_s
+        self._q: List[_GenRequest] = []
+        self._qlock = threading.Lock()
+        self._run = threading.Lock()
+        self.batch_sizes: List[int] = []
+
+    def _take(self) -> List[_GenRequest]:
+        with self._qlock:
+            if not self._q:
+                return []
+            neg = self._q[0].negative
+            batch, n, rest = [], 0, []
+            for r in self._q:
+                if r.negative == neg and (not batch or n + len(r.prompts) <= self.max_batch):
+                    batch.append(r)
+                    n += len(r.prompts)
+                else:
+                    rest.append(r)
+            self._q = rest
+            return batch
+
+    def generate(self, prompts, negative_prompt, seeds):
+        req = _GenRequest(prompts, negative_prompt, seeds)
+        with self._qlock:
+            self._q.append(req)
+        while not req.done.is_set():
+            if not self._run.acquire(timeout=0.005):
+                continue
+            try:
+                if req.done.is_set():
+                    break
+                if self.window_s > 0:
+                    time.sleep(self.window_s)      # let concurrent rooms join this batch
+                batch = self._take()
+                if not batch:
+                    continue
+                self.batch_sizes.append(sum(len(r.prompts) for r in batch))
+                try:
+                    imgs = self.inner.generate([p for r in batch for p in r.prompts], batch[0].negative,
+                                               [s for r in batch for s in r.seeds])
+                    i = 0
+                    for r in batch:
+                        r.result = imgs[i:i + len(r.prompts)]
+                        i += len(r.prompts)
+                except BaseException as e:  # noqa: BLE001 - every room of the batch sees the failure
+                    for r in batch:
+                        r.error = e
+                for r in batch:
+                    r.done.set()
+            finally:
+                self._run.release()
+        if req.error is not None:
+            raise req.error
+        return req.result

@@ -45,6 +45,56 @@ def _use_hip(t: torch.Tensor) -> bool:
     return True
 
 
+# ----------------------------------------------------------------------------- GEMM tuning
+# Measured per-shape plans (tools/autotune_gemm.py -> gemm_tuning.json): shape key -> (tile
+# config, split-K), consulted by the C++ planner before its cost model.  The recorder lets the
+# autotuner re-run every GEMM/conv launch of a real pipeline pass with identical arguments.
+_TUNE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_RECORD: Optional[list] = None
+_tune_loaded = False
+
+
+def load_gemm_tuning(path: Optional[str] = None) -> int:
+    """Load the tuning table into the extension (once per process unless a path is given).
+    ``CASSMANTLE_GEMM_TUNE=0`` disables it.  Returns the number of entries."""
+    global _tune_loaded
+    if os.environ.get("CASSMANTLE_GEMM_TUNE", "1") == "0" or not ext_available():
+        return 0
+    if _tune_loaded and path is None:
+        return ext().gemm_tune_size()
+    import json
+    p = path or _TUNE_PATH
+    _tune_loaded = True
+    if not os.path.exists(p):
+        return 0
+    with open(p) as f:
+        data = json.load(f)
+    for e in data.get("entries", []):
+        ext().gemm_tune_set(e["key"], int(e["cfg"]), int(e["split"]))
+    return ext().gemm_tune_size()
+
+
+def record_gemms(on: bool) -> Optional[list]:
+    """Start (``on``) / stop recording HIP GEMM & conv launches: each entry is
+    ``(key, closure)`` where the closure re-launches the same call.  Returns the list on stop."""
+    global _RECORD
+    if on:
+        _RECORD = []
+        ext().gemm_record_keys(True)
+        return _RECORD
+    rec, _RECORD = _RECORD, None
+    ext().gemm_record_keys(False)
+    return rec
+
+
+def _launch(fn, *args):
+    if not _tune_loaded:
+        load_gemm_tuning()
+    fn(*args)
+    if _RECORD is not None:
+        _RECORD.append((ext().gemm_last_key(), lambda: fn(*args)))
+
+
 _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5, "swiglu": 6}
 
 
@@ -106,7 +156,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
     r2 = residual.reshape(-1, N) if residual is not None else None
     hw = x2.shape[0] // x.shape[0] if stats is not None else 0
-    ext().gemm(x2, w, bias, r2, out, _ACT[act], stats, hw)
+    _launch(ext().gemm, x2, w, bias, r2, out, _ACT[act], stats, hw)
     return out.reshape(*x.shape[:-1], N)
 
 
@@ -157,7 +207,7 @@ def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.
     N = wf.shape[0] // 2 if act in ("geglu", "swiglu") else wf.shape[0]
     out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
     r2 = residual.reshape(rows, N) if residual is not None else None
-    ext().gemm(x2, wf, bf, r2, out, _ACT[act], None, 0, st, wsum)
+    _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, st, wsum)
     return out.reshape(*x.shape[:-1], N)
 
 
@@ -175,7 +225,8 @@ def linear_cat(x: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
     r2 = residual.reshape(rows, N) if residual is not None else None
     hw = rows // x.shape[0] if stats is not None else 0
-    ext().gemm_cat(x.reshape(rows, Ca).contiguous(), x2.reshape(rows, K - Ca).contiguous(), w, bias, r2, out, stats, hw)
+    _launch(ext().gemm_cat, x.reshape(rows, Ca).contiguous(), x2.reshape(rows, K - Ca).contiguous(), w, bias, r2, out,
+            stats, hw)
     return out.reshape(*x.shape[:-1], N)
 
 
@@ -228,7 +279,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     Ho = (Hi + 2 * padding - kh) // stride + 1
     Wo = (Wi + 2 * padding - kw) // stride + 1
     out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=x.dtype)
-    ext().conv2d(x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample), stats)
+    _launch(ext().conv2d, x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample), stats)
     return out
 
 
@@ -262,7 +313,7 @@ def conv2d_up2(x: torch.Tensor, w: torch.Tensor, w4: Optional[torch.Tensor] = No
     if w4 is None:
         w4 = fold_upsample_weights(w)
     out = torch.empty((B, 2 * H, 2 * W, w.shape[0]), device=x.device, dtype=x.dtype)
-    ext().conv2d_up2(x.contiguous(), w4, bias, residual, chan_bias, out, stats)
+    _launch(ext().conv2d_up2, x.contiguous(), w4, bias, residual, chan_bias, out, stats)
     return out
 
 

@@ -528,6 +528,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_cat", &gemm_cat);
   m.def("group_norm_cat", &group_norm_cat);
   m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });
+  m.def("gemm_tune_set", [](const std::string& key, int64_t cfg, int64_t split) { gemm_tune_set(key, (int)cfg, (int)split); });
+  m.def("gemm_tune_clear", []() { gemm_tune_clear(); });
+  m.def("gemm_tune_size", []() { return (int64_t)gemm_tune_size(); });
+  m.def("gemm_record_keys", [](bool on) { gemm_record_keys(on); });
+  m.def("gemm_last_key", []() { return gemm_last_key(); });
+  m.def("gemm_last_plan", []() { int c, sp; gemm_last_plan(&c, &sp); return std::vector<int64_t>{c, sp}; });
   m.def("gemm_rms", &gemm_rms);
   m.def("conv2d", &conv2d);
   m.def("conv2d_up2", &conv2d_up2);

@@ -1,6 +1,11 @@
 // MFMA GEMM / implicit-GEMM conv: tile planner and dispatch (kernels: gemm_impl.h, instantiated
 // per A-operand mode in gemm_c*.hip).
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <mutex>
+#include <string>
+#include <unordered_map>
 
 #include "common.h"
 #include "kernels.h"
@@ -11,6 +16,8 @@ void gemm_c1_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_c2_buf_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_c3_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_pp_c0_launch(const GemmArgs& p, float* ws, hipStream_t s);
+void gemm_pp_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
 
 namespace {
 
@@ -20,14 +27,23 @@ constexpr int BK = 64;
 //   0: 128x128 (2x2)   1: 128x160 (2x2, wave 80x64)   2: 256x64 (4x1)   3: 128x64 (2x2)   4: 256x16 (4x1)
 // 8 waves, 1 block per CU, 3-stage ring:
 //   5: 256x160 (4x2, wave 64x80)   6: 256x128 (4x2, wave 64x64)
+// 8-wave ping-pong kernel (gemm_pp.h; 1 block per CU, 4 phases per k-tile, counted vmcnt):
+//   7: 256x256   8: 256x160   9: 256x128   10: 128x256
+// deep LDS ring (gemm_impl.h STAGES 4-5, one block per CU; buffer-resource modes, bf16 out):
+//   11: 128x160 4w S4   12: 128x128 4w S4 (also gated)   13: 128x64 4w S5   14: 128x160 8w S4
+// Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 7;
+constexpr int kNumTiles = 15;
+constexpr int kFirstPP = 7;
+constexpr int kFirstDeep = 11;
 // slots = resident blocks on the chip: 128x64 needs 48 KiB of LDS per block, so 3 blocks fit a
 // CU (768 slots); with 512 the model undercounted it and missed the measured best on the
 // level-2..4 plain GEMMs (profiles/r1_gemm_plan_sweep.jsonl: 14.5 vs 17.8 us at 8192x640x640)
 constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f, 512}, {256, 64, 0.95f, 512},
                                        {128, 64, 0.80f, 768},  {256, 16, 0.25f, 512},  {256, 160, 1.02f, 256},
-                                       {256, 128, 1.00f, 256}};
+                                       {256, 128, 1.00f, 256}, {256, 256, 1.60f, 256}, {256, 160, 1.55f, 256},
+                                       {256, 128, 1.45f, 256}, {128, 256, 1.45f, 256}, {128, 160, 1.f, 256},
+                                       {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
@@ -91,7 +107,55 @@ __global__ void gemm_simt_kernel(GemmArgs p) {
     reinterpret_cast<uint16_t*>(p.C)[(long long)batch * p.sC + (long long)m * p.ldc + n] = f2bf(o);
 }
 
+// the ping-pong kernel takes the buffer-resource modes (plain / two-source A, Cin % 64 convs
+// without the fused upsample) with bf16 output
+bool pp_ok(const GemmArgs& p) {
+  // bf16 outputs the LDS-staged epilogue takes (the kernel's direct path only stores split-K slabs)
+  const int cbs = p.ldcb ? p.ldcb : p.N;
+  if (p.N % 8 != 0 || p.ldc % 8 != 0 || cbs % 4 != 0) return false;
+  if (p.out_f32 || !buf_ok(p) || p.K % BK != 0) return false;
+  if (p.conv && (p.upsample || p.Cin % 64 != 0)) return false;
+  return p.N > 16;
+}
+
+bool deep_ok(const GemmArgs& p) {
+  return !p.out_f32 && buf_ok(p) && p.K % BK == 0 && (!p.conv || (!p.upsample && p.Cin % 64 == 0)) && p.N > 16;
+}
+
+// ---- measured per-shape tuning table (tools/autotune_gemm.py -> ops/gemm_tuning.json, loaded by
+// ops/__init__.py): shape key -> (tile config, split-K).  Consulted before the cost model.
+std::mutex g_tune_mu;
+std::unordered_map<std::string, GemmPlan> g_tune;
+std::string g_last_key;
+GemmPlan g_last_plan{0, 1};
+bool g_record_key = false;
+
 }  // namespace
+
+std::string gemm_key(const GemmArgs& p) {
+  char buf[192];
+  snprintf(buf, sizeof(buf), "m%d n%d k%d w%d b%d c%d:%d:%d:%d:%d:%d:%d:%d p%d a%d g%d s%d r%d cb%d ln%d f%d",
+           p.M, p.N, p.K, p.Nw, p.batch, p.conv, p.IH, p.IW, p.Cin, p.stride, p.ksize, p.pad, p.upsample, p.parity,
+           p.A2 != nullptr, is_gated(p.act) ? 1 : 0, p.stats != nullptr, p.residual != nullptr, p.chan_bias != nullptr,
+           p.ln_rows != nullptr, p.out_f32);
+  return std::string(buf);
+}
+
+void gemm_tune_set(const std::string& key, int cfg, int split) {
+  std::lock_guard<std::mutex> g(g_tune_mu);
+  g_tune[key] = GemmPlan{cfg, split};
+}
+void gemm_tune_clear() {
+  std::lock_guard<std::mutex> g(g_tune_mu);
+  g_tune.clear();
+}
+int gemm_tune_size() {
+  std::lock_guard<std::mutex> g(g_tune_mu);
+  return (int)g_tune.size();
+}
+void gemm_record_keys(bool on) { g_record_key = on; }
+std::string gemm_last_key() { return g_last_key; }
+void gemm_last_plan(int* cfg, int* split) { *cfg = g_last_plan.cfg; *split = g_last_plan.split; }
 
 // Choose tile config + split-K by an occupancy-round cost model: the kernel is latency-bound
 // per k-tile, so time ~ rounds(blocks / 512) x k-tiles-per-block x tile-cost; split-K adds a
@@ -110,31 +174,67 @@ void gemm_set_override(int cfg, int split) {
   g_force_split = split;
 }
 
+static GemmPlan gemm_plan_impl(const GemmArgs& p);
 GemmPlan gemm_plan(const GemmArgs& p) {
+  const GemmPlan r = gemm_plan_impl(p);
+  if (g_record_key) g_last_plan = r;
+  return r;
+}
+
+static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   GemmPlan best{0, 1};
   if (g_force_cfg == -2) {
     g_force_cfg = env_int("CASSMANTLE_GEMM_CFG", -1);
     g_force_split = env_int("CASSMANTLE_GEMM_SPLIT", 0);
   }
   const int force_cfg = g_force_cfg, force_split = g_force_split;
+  if (g_record_key) g_last_key = gemm_key(p);
+  if (force_cfg < 0) {
+    bool have = false;
+    GemmPlan tp{0, 1};
+    {
+      std::lock_guard<std::mutex> g(g_tune_mu);
+      if (!g_tune.empty()) {
+        auto it = g_tune.find(gemm_key(p));
+        if (it != g_tune.end()) { tp = it->second; have = true; }
+      }
+    }
+    // a table entry is only taken if the kernel family can run this call (same checks as a
+    // forced config), so a stale table never selects an unsupported path
+    if (have && (tp.cfg < kFirstPP || (tp.cfg < kFirstDeep ? pp_ok(p) : deep_ok(p)))) return tp;
+  }
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
   const bool gated = p.act == ACT_GEGLU || p.act == ACT_SWIGLU;
   int only = -1;                         // forced tile (cost model still picks the split)
-  if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16))) {
+  const bool pp_elig = pp_ok(p);
+  // CASSMANTLE_GEMM_PP=0 keeps the planner on the 4-wave kernel (A/B knob); forced configs
+  // (CASSMANTLE_GEMM_CFG / gemm_set_override) only need eligibility
+  static const int pp_auto = env_int("CASSMANTLE_GEMM_PP", 0);
+  const bool pp = pp_elig && pp_auto;
+  const bool deep_elig = deep_ok(p);
+  if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
+      (force_cfg < kFirstPP || (force_cfg < kFirstDeep ? pp_elig : deep_elig))) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
+      else if (force_cfg >= kFirstDeep) best.cfg = 12;            // the deep-ring gated tile
+      else if (force_cfg >= kFirstPP) best.cfg = 9;               // the ping-pong gated tile
       return best;
     }
     only = force_cfg;
   }
-  if (gated) return best;
+  if (gated) {
+    if (pp && (p.N % 64 == 0) && (long long)(p.N / 64) * ((p.M + 255) / 256) >= 256) best.cfg = 9;
+    return best;
+  }
   const int nk = (p.K + BK - 1) / BK;
   // M <= 8 goes to the GEMV path; short prompts (M = tens of rows) need split-K to fill the chip
   const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M > 8;
   double best_t = 1e30;
   for (int c = 0; c < kNumTiles; ++c) {
     const TileCfg& tc = kTiles[c];
-    if (only >= 0 ? c != only : (c >= 5 && !use_big)) continue;
+    if (only >= 0 ? c != only : ((c == 5 || c == 6) && !use_big)) continue;
+    if (c >= kFirstDeep && only != c) continue;   // table / forced only
+    if (c >= kFirstPP && c < kFirstDeep && !(only >= 0 ? pp_elig : pp)) continue;
     if (c == 4 && p.N > 16) continue;
     if (c != 4 && p.N <= 16) continue;
     const long long tiles = (long long)((p.N + tc.BN - 1) / tc.BN) * ((p.M + tc.BM - 1) / tc.BM) * p.batch;
@@ -175,6 +275,11 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     return;
   }
   const bool buf = buf_ok(p);
+  if (p.cfg >= kFirstPP && p.cfg < kFirstDeep && pp_ok(p)) {
+    if (!p.conv) gemm_pp_c0_launch(p, ws, s);
+    else gemm_pp_c2_launch(p, ws, s);
+    return;
+  }
   if (!p.conv) {
     if (buf) gemm_c0_buf_launch(p, ws, s);
     else gemm_c0_launch(p, ws, s);

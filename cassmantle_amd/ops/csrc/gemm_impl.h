@@ -129,11 +129,243 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   }
 }
 
-// 4-wave blocks run 2 per CU (2 LDS stages); 8-wave blocks (256-row tiles) run 1 per CU with a
-// 3-stage ring: two k-tiles of DMA stay in flight across every barrier while the 2 waves per
-// SIMD alternate MFMA and LDS work.
+// Per-fragment forms of the direct epilogue.  They stay INLINE: an out-of-line call gives the
+// kernel a stack (scratch) and measured 1.5-2x slower on every GEMM; the unrolled loop they sit
+// in exceeds the default pragma-unroll size limit, so build.py raises it
+// (-mllvm -pragma-unroll-threshold) rather than let the accumulators go to scratch.
+template <bool OUTF32>
+CM_DEVICE void epilogue4_call(const GemmArgs& p, int batch, int m, int n, f32x4_t v) {
+  float o[4] = {v[0], v[1], v[2], v[3]};
+  epilogue4<OUTF32>(p, batch, m, n, o);
+}
+
+CM_DEVICE void gated_epilogue4_call(const GemmArgs& p, int batch, int m, int n, f32x4_t hv, f32x4_t gv) {
+  float o[4], hh[4] = {hv[0], hv[1], hv[2], hv[3]}, gg[4] = {gv[0], gv[1], gv[2], gv[3]};
+  if (p.ln_rows) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float h = hh[r], g = gg[r];
+    if (p.bias) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
+    o[r] = gate_f(h, g, p.act);
+  }
+  uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
+  if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
+  *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+}
+
+// Shared tile epilogue of the MFMA GEMM kernels: acc[TI][TJ] holds, for W subtile i and A
+// subtile j of wave (wm, wn), D[n][m] with n = n0 + wn*(BN/WN) + 16i + 4*(lane>>4) + r and
+// m = m0 + wm*(BM/WM) + 16j + (lane&15).  bf16 outputs without split are staged through LDS
+// (smem, >= BM*(OBN+8)*2 bytes) and stored as full 16-byte row chunks (+ residual, + GroupNorm
+// statistics); fp32 / split-K / ragged outputs take the direct path.
+// SPLIT_DIRECT: the caller guarantees the direct path only ever stores split-K partial slabs
+// (bf16, N % 8 == 0 outputs always take the LDS path), which keeps the kernel small.
+template <int BM, int BN, int WM, int WN, bool GEGLU, bool OUTF32, int TI, int TJ, int THREADS, bool SPLIT_DIRECT = false>
+CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* smem, float* __restrict__ partial,
+                             int m0, int n0, int batch, int wm, int wn, int tid, int nsplit, int split_id) {
+  const int lane = tid & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  // ---- LDS-staged epilogue (bf16 output, no split): the MFMA layout gives each lane 4
+  // consecutive columns of one row (8-byte stores, 32 B per row per instruction); instead the
+  // tile is written to LDS (bias / time-bias / activation applied in registers) and streamed out
+  // as full rows of 16-byte stores, residual added in the same coalesced pass.
+  if constexpr (!OUTF32) {
+    constexpr int OBN = GEGLU ? BN / 2 : BN;   // output columns of this tile
+    constexpr int OST = OBN + 8;               // LDS row stride (elements): 16-B pad
+    const long long cbs = p.ldcb ? p.ldcb : p.N;
+    const bool lds_ok = nsplit == 1 && (p.N % 8 == 0) && (p.ldc % 8 == 0) && (cbs % 4 == 0);
+    if (lds_ok) {
+      __syncthreads();                        // every wave is done with the staging buffers
+      uint16_t* T = reinterpret_cast<uint16_t*>(smem);
+      const int hw = p.Ho * p.Wo;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int ml = wm * (BM / WM) + 16 * j + fr;
+        const int m = m0 + ml;
+        const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
+        if constexpr (GEGLU) {
+#pragma unroll
+          for (int pi = 0; pi < TI / 2; ++pi) {
+            const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;
+            const int n = n0 + nl;
+            float o[4], hh[4], gg[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
+            if (p.ln_rows && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float h = hh[r], g = gg[r];
+              if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
+              o[r] = gate_f(h, g, p.act);
+            }
+            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) {
+            const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
+            const int n = n0 + nl;
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (p.ln_rows && n < p.N && m < p.M) ln_fold4(p, m, n, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
+            if (n < p.N && m < p.M) {
+              if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
+              if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
+              if (p.act != ACT_NONE) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
+              }
+            }
+            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+        }
+      }
+      __syncthreads();
+      constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
+      uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
+      auto finish = [&](int row, int c8) -> uint4 {   // residual add + store of one 16-B chunk
+        const int m = m0 + row, n = n0 + c8 * 8;
+        const long long om = out_row(p, m, batch);
+        uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
+        if (p.residual) {
+          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + om * p.ldc + n);
+          float a[8], b[8];
+          unpack8(v, a);
+          unpack8(rv, b);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += b[e];
+          v = pack8(a);
+        }
+        *reinterpret_cast<uint4*>(Cb + om * p.ldc + n) = v;
+        return v;
+      };
+      if (p.stats == nullptr) {
+        for (int c = tid; c < BM * CPR; c += THREADS) {
+          const int row = c / CPR, c8 = c - row * CPR;
+          if (m0 + row >= p.M || n0 + c8 * 8 >= p.N) continue;
+          finish(row, c8);
+        }
+        return;
+      }
+      // GroupNorm statistics of the stored output (consumer: group_norm with stats): each thread
+      // owns one 8-column chunk and walks rows; per-(image, column) sum / sum-of-squares are
+      // reduced over the row lanes in LDS and added to p.stats[image][n][2] with one atomic per
+      // column per tile (tiles that straddle images flush per thread instead).
+      constexpr int RL = THREADS / CPR;          // row lanes
+      const int c8 = tid % CPR, r0 = tid / CPR;
+      const int n = n0 + c8 * 8;
+      const bool lane_on = r0 < RL && n < p.N;
+      const int shw = p.stats_hw;
+      const int mlast = min(m0 + BM, p.M) - 1;
+      const int img0 = m0 / shw;
+      const bool single = img0 == mlast / shw;
+      float s8[8], q8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
+      int cur = -1;
+      auto flush = [&]() {
+        if (cur < 0) return;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, 0, s8[e]);
+          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, 1, q8[e]);
+          s8[e] = 0.f;
+          q8[e] = 0.f;
+        }
+      };
+      if (lane_on) {
+        for (int row = r0; row < BM; row += RL) {
+          const int m = m0 + row;
+          if (m >= p.M) break;
+          const uint4 v = finish(row, c8);
+          if (!single) {
+            const int img = m / shw;
+            if (img != cur) { flush(); cur = img; }
+          }
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s8[e] += f[e]; q8[e] = fmaf(f[e], f[e], q8[e]); }
+        }
+      }
+      if (!single) {
+        flush();
+        return;
+      }
+      __syncthreads();                          // T fully consumed: reuse LDS for the reduction
+      float* R = reinterpret_cast<float*>(smem);   // [2][RL][OBN]
+      if (r0 < RL) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          R[r0 * OBN + c8 * 8 + e] = s8[e];
+          R[(RL + r0) * OBN + c8 * 8 + e] = q8[e];
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < 2 * OBN; c += THREADS) {
+        const int stat = c / OBN, col = c - stat * OBN;
+        if (n0 + col >= p.N) continue;
+        float a = 0.f;
+        for (int r = 0; r < RL; ++r) a += R[(stat * RL + r) * OBN + col];
+        stat_atomic_add(p.stats + ((long long)img0 * p.N + n0 + col) * 2 + stat, stat, a);
+      }
+      return;
+    }
+  }
+
+  // ---- direct epilogue (fp32 outputs, split-K partial slabs, ragged N)
+  if constexpr (SPLIT_DIRECT) {
+    if constexpr (!GEGLU) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int m = m0 + wm * (BM / WM) + 16 * j + fr;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
+          if (m < p.M && n < p.N) {
+            float* dst = partial + ((long long)split_id * p.M + m) * p.N + n;
+            *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+          }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int m = m0 + wm * (BM / WM) + 16 * j + fr;
+    if (m >= p.M) continue;
+    if constexpr (GEGLU) {
+#pragma unroll
+      for (int pi = 0; pi < TI / 2; ++pi) {
+        const int n = n0 + wn * (BN / WN / 2) + 16 * pi + 4 * fq;
+        if (n >= p.N) continue;
+        gated_epilogue4_call(p, batch, m, n, acc[2 * pi][j], acc[2 * pi + 1][j]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
+        if (n >= p.N) continue;
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (nsplit > 1) {               // split-K: raw fp32 partial slab
+          float* dst = partial + ((long long)split_id * p.M + m) * p.N + n;
+          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+          epilogue4_call<OUTF32>(p, batch, m, n, acc[i][j]);
+        }
+      }
+    }
+  }
+}
+
+// 4-wave blocks with 2 LDS stages run 2 per CU; deeper rings (STAGES 3-5, one block per CU)
+// keep STAGES-2 k-tiles of DMA in flight across every barrier: the short-K / small-grid UNet
+// GEMMs (K = 320..1280, <= 2 tiles per CU) are bound by the per-k-tile DMA latency, not by
+// MFMA, and a 2-stage loop exposes that latency once per k-tile.
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
-__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1)
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 && STAGES == 2) ? 2 : 1)
 gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int NW = WM * WN;
@@ -147,12 +379,12 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   static_assert(BM % RR == 0, "A rows in whole DMA rounds");
   constexpr int AR = BM / RR;              // A DMA rounds
   constexpr int WR = (BN + RR - 1) / RR;   // W DMA rounds (the last may cover only some waves)
-  static_assert(STAGES == 2 || STAGES == 3, "stages");
+  static_assert(STAGES >= 2 && STAGES <= 5, "stages");
   constexpr int NPT = AR + WR;             // DMA instructions per k-tile of a wave in every round
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int wm = wave % WM, wn = wave / WM;
 
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
@@ -433,210 +665,36 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       __syncthreads();
     }
   } else {
-    if (nk > 0) stage(kt0, 0);
-    if (nk > 1) stage(kt0 + 1, 1);
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) {                    // retire tile t, leave tile t+1 in flight
-        if (w_last_round) wait_vmcnt<NPT>();
-        else wait_vmcnt<NPT - 1>();
+    // STAGES-deep ring: tiles t+1 .. t+STAGES-2 stay in flight while tile t is consumed
+    constexpr int S = STAGES;
+    const int npt = w_last_round ? NPT : NPT - 1;   // this wave's DMAs per k-tile (uniform)
+    auto wait_tiles = [&](int k) {                  // leave k tiles' DMAs outstanding
+      if (npt == NPT) {
+        if (k <= 0) wait_vmcnt<0>();
+        else if (k == 1) wait_vmcnt<NPT>();
+        else if (k == 2) wait_vmcnt<2 * NPT>();
+        else wait_vmcnt<3 * NPT>();
       } else {
-        wait_vmcnt<0>();
+        if (k <= 0) wait_vmcnt<0>();
+        else if (k == 1) wait_vmcnt<NPT - 1>();
+        else if (k == 2) wait_vmcnt<2 * (NPT - 1)>();
+        else wait_vmcnt<3 * (NPT - 1)>();
       }
+    };
+#pragma unroll
+    for (int s0 = 0; s0 < S - 1; ++s0)
+      if (s0 < nk) stage(kt0 + s0, s0);
+    for (int t = 0; t < nk; ++t) {
+      wait_tiles(min(S - 2, nk - 1 - t));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();        // every wave's share of tile t landed; tile t-1 is free
-      if (t + 2 < nk) stage(kt0 + t + 2, (t + 2) % 3);
-      compute(t % 3);
+      if (t + S - 1 < nk) stage(kt0 + t + S - 1, (t + S - 1) % S);
+      compute(t % S);
     }
   }
 
-  // ---- LDS-staged epilogue (bf16 output, no split): the MFMA layout gives each lane 4
-  // consecutive columns of one row (8-byte stores, 32 B per row per instruction); instead the
-  // tile is written to LDS (bias / time-bias / activation applied in registers) and streamed out
-  // as full rows of 16-byte stores, residual added in the same coalesced pass.
-  if constexpr (!OUTF32) {
-    constexpr int OBN = GEGLU ? BN / 2 : BN;   // output columns of this tile
-    constexpr int OST = OBN + 8;               // LDS row stride (elements): 16-B pad
-    const long long cbs = p.ldcb ? p.ldcb : p.N;
-    const bool lds_ok = gridDim.y == 1 && (p.N % 8 == 0) && (p.ldc % 8 == 0) && (cbs % 4 == 0);
-    if (lds_ok) {
-      __syncthreads();                        // every wave is done with the staging buffers
-      uint16_t* T = reinterpret_cast<uint16_t*>(smem);
-      const int hw = p.Ho * p.Wo;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int ml = wm * (BM / WM) + 16 * j + fr;
-        const int m = m0 + ml;
-        const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
-        if constexpr (GEGLU) {
-#pragma unroll
-          for (int pi = 0; pi < TI / 2; ++pi) {
-            const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;
-            const int n = n0 + nl;
-            float o[4], hh[4], gg[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
-            if (p.ln_rows && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float h = hh[r], g = gg[r];
-              if (p.bias && n < p.N) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-              o[r] = gate_f(h, g, p.act);
-            }
-            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < TI; ++i) {
-            const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
-            const int n = n0 + nl;
-            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (p.ln_rows && n < p.N && m < p.M) ln_fold4(p, m, n, o);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
-            if (n < p.N && m < p.M) {
-              if (p.bias) add4(o, *reinterpret_cast<const uint2*>(p.bias + n));
-              if (p.chan_bias) add4(o, *reinterpret_cast<const uint2*>(p.chan_bias + (long long)bimg * cbs + n));
-              if (p.act != ACT_NONE) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
-              }
-            }
-            *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          }
-        }
-      }
-      __syncthreads();
-      constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
-      uint16_t* Cb = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC;
-      auto finish = [&](int row, int c8) -> uint4 {   // residual add + store of one 16-B chunk
-        const int m = m0 + row, n = n0 + c8 * 8;
-        const long long om = out_row(p, m, batch);
-        uint4 v = *reinterpret_cast<const uint4*>(T + row * OST + c8 * 8);
-        if (p.residual) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(p.residual + om * p.ldc + n);
-          float a[8], b[8];
-          unpack8(v, a);
-          unpack8(rv, b);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[e] += b[e];
-          v = pack8(a);
-        }
-        *reinterpret_cast<uint4*>(Cb + om * p.ldc + n) = v;
-        return v;
-      };
-      if (p.stats == nullptr) {
-        for (int c = tid; c < BM * CPR; c += THREADS) {
-          const int row = c / CPR, c8 = c - row * CPR;
-          if (m0 + row >= p.M || n0 + c8 * 8 >= p.N) continue;
-          finish(row, c8);
-        }
-        return;
-      }
-      // GroupNorm statistics of the stored output (consumer: group_norm with stats): each thread
-      // owns one 8-column chunk and walks rows; per-(image, column) sum / sum-of-squares are
-      // reduced over the row lanes in LDS and added to p.stats[image][n][2] with one atomic per
-      // column per tile (tiles that straddle images flush per thread instead).
-      constexpr int RL = THREADS / CPR;          // row lanes
-      const int c8 = tid % CPR, r0 = tid / CPR;
-      const int n = n0 + c8 * 8;
-      const bool lane_on = r0 < RL && n < p.N;
-      const int shw = p.stats_hw;
-      const int mlast = min(m0 + BM, p.M) - 1;
-      const int img0 = m0 / shw;
-      const bool single = img0 == mlast / shw;
-      float s8[8], q8[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
-      int cur = -1;
-      auto flush = [&]() {
-        if (cur < 0) return;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 0, 0, s8[e]);
-          stat_atomic_add(p.stats + ((long long)cur * p.N + n + e) * 2 + 1, 1, q8[e]);
-          s8[e] = 0.f;
-          q8[e] = 0.f;
-        }
-      };
-      if (lane_on) {
-        for (int row = r0; row < BM; row += RL) {
-          const int m = m0 + row;
-          if (m >= p.M) break;
-          const uint4 v = finish(row, c8);
-          if (!single) {
-            const int img = m / shw;
-            if (img != cur) { flush(); cur = img; }
-          }
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { s8[e] += f[e]; q8[e] = fmaf(f[e], f[e], q8[e]); }
-        }
-      }
-      if (!single) {
-        flush();
-        return;
-      }
-      __syncthreads();                          // T fully consumed: reuse LDS for the reduction
-      float* R = reinterpret_cast<float*>(smem);   // [2][RL][OBN]
-      if (r0 < RL) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          R[r0 * OBN + c8 * 8 + e] = s8[e];
-          R[(RL + r0) * OBN + c8 * 8 + e] = q8[e];
-        }
-      }
-      __syncthreads();
-      for (int c = tid; c < 2 * OBN; c += THREADS) {
-        const int stat = c / OBN, col = c - stat * OBN;
-        if (n0 + col >= p.N) continue;
-        float a = 0.f;
-        for (int r = 0; r < RL; ++r) a += R[(stat * RL + r) * OBN + col];
-        stat_atomic_add(p.stats + ((long long)img0 * p.N + n0 + col) * 2 + stat, stat, a);
-      }
-      return;
-    }
-  }
-
-  // ---- direct epilogue (fp32 outputs, split-K partial slabs, ragged N)
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int m = m0 + wm * (BM / WM) + 16 * j + fr;
-    if (m >= p.M) continue;
-    if constexpr (GEGLU) {
-#pragma unroll
-      for (int pi = 0; pi < TI / 2; ++pi) {
-        const int n = n0 + wn * (BN / WN / 2) + 16 * pi + 4 * fq;
-        if (n >= p.N) continue;
-        float o[4], hh[4], gg[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
-        if (p.ln_rows) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float h = hh[r], g = gg[r];
-          if (p.bias) { h += bf2f(p.bias[n + r]); g += bf2f(p.bias[p.N + n + r]); }
-          o[r] = gate_f(h, g, p.act);
-        }
-        uint16_t* C = reinterpret_cast<uint16_t*>(p.C) + (long long)batch * p.sC + (long long)m * p.ldc + n;
-        if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n));
-        *reinterpret_cast<uint2*>(C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
-        if (n >= p.N) continue;
-        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (gridDim.y > 1) {               // split-K: raw fp32 partial slab
-          float* dst = partial + ((long long)blockIdx.y * p.M + m) * p.N + n;
-          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
-          epilogue4<OUTF32>(p, batch, m, n, o);
-        }
-      }
-    }
-  }
+  tile_epilogue<BM, BN, WM, WN, GEGLU, OUTF32, TI, TJ, THREADS>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
+                                                               gridDim.y, blockIdx.y);
 }
 
 // split-K: a second, fully parallel pass sums the slices' fp32 slabs and applies the epilogue
@@ -807,6 +865,16 @@ void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
 
 template <int CONV, bool OUTF32, bool BUF>
 void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
+  // deep-ring tiles (buffer-resource modes, bf16 out): one block per CU, STAGES-2 k-tiles ahead
+  if constexpr (BUF && !OUTF32) {
+    switch (p.cfg) {
+      case 11: return launch_t<128, 160, 2, 2, CONV, false, false, 4, true>(p, ws, s);
+      case 12: return launch_t<128, 128, 2, 2, CONV, false, false, 4, true>(p, ws, s);
+      case 13: return launch_t<128, 64, 2, 2, CONV, false, false, 5, true>(p, ws, s);
+      case 14: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true>(p, ws, s);
+      default: break;
+    }
+  }
   switch (p.cfg) {
     case 1: launch_st<128, 160, 2, 2, CONV, false, OUTF32, BUF>(p, ws, s); break;
     case 2: launch_st<256, 64, 4, 1, CONV, false, OUTF32, BUF>(p, ws, s); break;
@@ -821,6 +889,9 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
 template <int CONV, bool BUF>
 void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
   if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) {
+    if constexpr (BUF) {
+      if (p.cfg == 12) return launch_t<128, 128, 2, 2, CONV, true, false, 4, true>(p, ws, s);
+    }
     if (p.cfg == 6) launch_st<256, 128, 4, 2, CONV, true, false, BUF>(p, ws, s);
     else launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);
   }

@@ -51,6 +51,15 @@ GemmPlan gemm_plan(const GemmArgs& p);
 int gemm_plan_split(const GemmArgs& p);
 // force a tile config (-1: cost model) and split-K factor (0: cost model) for every later plan
 void gemm_set_override(int cfg, int split);
+// measured tuning table: shape key (gemm_key) -> plan; key recording for the autotuner
+#include <string>
+std::string gemm_key(const GemmArgs& p);
+void gemm_tune_set(const std::string& key, int cfg, int split);
+void gemm_tune_clear();
+int gemm_tune_size();
+void gemm_record_keys(bool on);
+std::string gemm_last_key();
+void gemm_last_plan(int* cfg, int* split);
 // ws: fp32 workspace of split * M * N floats when split > 1 (else may be null)
 void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s);
 

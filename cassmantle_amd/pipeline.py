@@ -15,6 +15,7 @@ hot loop of the whole framework, so:
 from __future__ import annotations
 
 import contextlib
+import threading
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -119,6 +120,14 @@ class StableDiffusion:
         # generation runs on its own stream (never the legacy default stream), so a serving
         # process can overlap it with the scorer's high-priority stream (BASELINE config 5)
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # one generation at a time per pipeline: the per-shape step state (latents, K/V context
+        # buffers, time table, captured graph) is shared, so concurrent callers (several rooms'
+        # worker threads) must not interleave (serving batches rooms through
+        # BatchingImageGenerator instead of queueing on this lock)
+        self._lock = threading.RLock()
+        # device flag: were the final latents of the last generation finite (checked before the
+        # uint8 decode, where NaN/Inf would silently become a garbage image)
+        self.last_finite: Optional[torch.Tensor] = None
 
     @property
     def latent_size(self) -> int:
@@ -212,6 +221,10 @@ class StableDiffusion:
         """-> uint8 [B, H, W, 3] on device (ordered before the caller's current stream)."""
         plan = make_plan(scheduler or self.spec.scheduler, steps or self.spec.steps,
                          self.spec.guidance if guidance is None else guidance)
+        with self._lock:
+            return self._generate_locked(prompts, negative, seeds, plan)
+
+    def _generate_locked(self, prompts, negative, seeds, plan) -> torch.Tensor:
         caller = torch.cuda.current_stream(self.device) if self.stream is not None else None
         with (torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()):
             if caller is not None:
@@ -223,6 +236,7 @@ class StableDiffusion:
             with span("denoise", self.stream):
                 x = self.denoise(ctx, x0, plan, added)
             with span("decode", self.stream):
+                self.last_finite = torch.isfinite(x).all()
                 img = self.vae.decode_uint8(x.to(self.dtype))
         if caller is not None:
             caller.wait_stream(self.stream)
@@ -230,10 +244,12 @@ class StableDiffusion:
         return img
 
     def generate(self, prompts: Sequence[str], negative: str, seeds: Sequence[int], **kw) -> List[np.ndarray]:
-        img = self.generate_tensor(prompts, negative, seeds, **kw)
-        arr = img.cpu().numpy()
-        if not np.isfinite(arr.astype(np.float32)).all():
-            raise ImageGenerationError("non-finite image")
+        with self._lock:
+            img = self.generate_tensor(prompts, negative, seeds, **kw)
+            finite = self.last_finite
+            arr = img.cpu().numpy()
+            if finite is not None and not bool(finite.item()):
+                raise ImageGenerationError("non-finite latents (NaN/Inf in the denoise loop)")
         return [arr[i] for i in range(arr.shape[0])]
 
 

@@ -370,3 +370,86 @@ def test_latent_step_matches_reference(sched):
                 ops.advance_step(step)
         state.append(x.cpu())
     assert rel_err(state[1], state[0]) < 1e-4
+
+
+# ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
+PP_CFGS = [7, 8, 9, 10, 11, 12, 13, 14]   # ping-pong (7-10) and deep-ring (11-14) tiles
+
+
+@pytest.fixture
+def force_cfg():
+    from cassmantle_amd.ops._ext import ext
+    yield lambda c, s=0: ext().gemm_set_override(c, s)
+    ext().gemm_set_override(-1, 0)
+
+
+@pytest.mark.parametrize("cfg", PP_CFGS)
+@pytest.mark.parametrize("M,N,K,split", [(1000, 320, 320, 1), (4096, 640, 1280, 1), (300, 1280, 2560, 4),
+                                         (77, 768, 768, 1), (2048, 200, 640, 2)])
+def test_gemm_pp_linear(cfg, M, N, K, split, force_cfg):
+    """every ping-pong tile (partial M / N tiles, tails of 1..5 k-tiles, split-K slabs) with bias,
+    residual and an activation vs the fp32 reference; asymmetric data catches layout swaps"""
+    x = rnd(M, K, seed=101)
+    w = rnd(N, K, scale=K ** -0.5, seed=102)
+    b = rnd(N, scale=0.1, seed=103)
+    r = rnd(M, N, seed=104)
+    force_cfg(cfg, split)
+    out = ops.linear(x, w, b, residual=r, act="silu")
+    exp = ref.linear(x, w, b, residual=r, act="silu")
+    assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", PP_CFGS)
+def test_gemm_pp_geglu_cat_stats(cfg, force_cfg):
+    force_cfg(cfg)
+    # gated (the planner maps every forced config to the 256x128 gated tile)
+    x = rnd(700, 320, seed=105)
+    w = rnd(2 * 640, 320, scale=320 ** -0.5, seed=106)
+    b = rnd(2 * 640, scale=0.1, seed=107)
+    assert rel_err(ops.linear(x, w, b, act="geglu"), ref.linear(x, w, b, act="geglu")) < 1e-2
+    # two-source A (channel concatenation) with fused GroupNorm statistics
+    B, HW, Ca, Cb, N = 2, 300, 640, 320, 320
+    a = rnd(B, HW, Ca, seed=108)
+    s2 = rnd(B, HW, Cb, seed=109)
+    w2 = rnd(N, Ca + Cb, scale=(Ca + Cb) ** -0.5, seed=110)
+    b2 = rnd(N, scale=0.1, seed=111)
+    st = ops.new_stats(B, N, DEV)
+    out = ops.linear_cat(a, s2, w2, b2, stats=st)
+    exp = ref.linear(torch.cat([a, s2], -1), w2, b2)
+    assert rel_err(out, exp) < 1e-2
+    exp_st = ops.new_stats(B, N, DEV)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", PP_CFGS)
+@pytest.mark.parametrize("B,H,W,Cin,Cout,stride", [(2, 17, 13, 64, 128, 1), (2, 16, 16, 320, 320, 2),
+                                                   (3, 12, 12, 128, 320, 1)])
+def test_conv_pp(cfg, B, H, W, Cin, Cout, stride, force_cfg):
+    x = rnd(B, H, W, Cin, seed=112)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=113)
+    b = rnd(Cout, scale=0.1, seed=114)
+    cb = rnd(B, Cout, scale=0.1, seed=115)
+    Ho = (H - 1) // stride + 1
+    Wo = (W - 1) // stride + 1
+    res = rnd(B, Ho, Wo, Cout, seed=116)
+    st = ops.new_stats(B, Cout, DEV)
+    force_cfg(cfg)
+    out = ops.conv2d(x, w, b, stride=stride, padding=1, residual=res, chan_bias=cb, stats=st)
+    exp = ref.conv2d(x, w, b, stride, 1, res, False, cb)
+    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
+    exp_st = ops.new_stats(B, Cout, DEV)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", PP_CFGS)
+def test_conv_up2_pp(cfg, force_cfg):
+    B, H, W, Cin, Cout = 2, 8, 12, 128, 192
+    x = rnd(B, H, W, Cin, seed=117)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=118)
+    b = rnd(Cout, scale=0.1, seed=119)
+    force_cfg(cfg)
+    out = ops.conv2d_up2(x, w, None, b)
+    exp = ref.conv2d(x, w, b, 1, 1, None, True, None)
+    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
