@@ -145,12 +145,15 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         if room is None:
             return JSONResponse({"error": "unknown room"}, status_code=404)
         t0 = time.perf_counter()
+        minted = None
         if not session_id:
-            # reference would key a session on None; give the caller a real session instead
-            session_id = str(uuid.uuid4())
+            # the reference keys such a request on a None session; here the caller gets a real
+            # session AND its cookie, so repeated cookie-less calls do not pile up orphans
+            session_id = minted = str(uuid.uuid4())
         if not room.session_exists(session_id):
             room.init_client(session_id)
-        jpeg = await asyncio.to_thread(room.fetch_masked_image, session_id)
+        # store reads on the loop; only the blur + JPEG encode runs in a worker thread
+        jpeg = await asyncio.to_thread(room.render_masked_image, room.masked_image_request(session_id))
         content = {
             "image": base64.b64encode(jpeg).decode(),
             "prompt": room.fetch_prompt_json(session_id),
@@ -158,7 +161,10 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         }
         counters["fetch_ms"] += (time.perf_counter() - t0) * 1e3
         counters["fetches"] += 1
-        return JSONResponse(content=content)
+        resp = JSONResponse(content=content)
+        if minted:
+            resp.set_cookie(key="session_id", value=minted)
+        return resp
 
     @app.post("/compute_score")
     async def compute_score(request: Request, session_id: Optional[str] = Cookie(None)):
@@ -168,8 +174,9 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         if room is None:
             return JSONResponse({"error": "unknown room"}, status_code=404)
         t0 = time.perf_counter()
+        minted = None
         if not session_id:
-            session_id = str(uuid.uuid4())
+            session_id = minted = str(uuid.uuid4())
         if not room.session_exists(session_id):
             room.init_client(session_id)
         try:
@@ -182,7 +189,10 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         scores = await room.compute_client_scores(session_id, {str(k): str(v) for k, v in inputs.items()})
         counters["score_ms"] += (time.perf_counter() - t0) * 1e3
         counters["scores"] += 1
-        return JSONResponse(scores)
+        resp = JSONResponse(scores)
+        if minted:
+            resp.set_cookie(key="session_id", value=minted)
+        return resp
 
     @app.get("/healthz")
     async def healthz():

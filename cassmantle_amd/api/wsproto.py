@@ -20,7 +20,9 @@ from urllib.parse import unquote
 
 log = logging.getLogger("cassmantle")
 _GUID = b"258EAFA5-E914-47DA-95CA-C5AB0DC85B11"
-MAX_MESSAGE = 1 << 20
+MAX_MESSAGE = 1 << 20          # largest frame AND largest reassembled message
+MAX_HANDSHAKE = 16 << 10       # request line + headers
+MAX_QUEUED = 64                # received messages not yet taken by the application
 
 
 def accept_key(key: bytes) -> bytes:
@@ -42,12 +44,17 @@ def encode_frame(opcode: int, payload: bytes, fin: bool = True) -> bytes:
 
 class FrameParser:
     """Incremental client-frame decoder.  ``feed`` returns complete (opcode, payload) messages
-    (continuations reassembled; control frames returned as they arrive)."""
+    (continuations reassembled; control frames returned as they arrive).  Raises ``ValueError``
+    (-> close 1002) on protocol errors: an unmasked client frame (RFC 6455 §5.1), a frame or a
+    reassembled message over ``MAX_MESSAGE``, a fragmented or oversized control frame, or a
+    continuation without a start."""
 
-    def __init__(self) -> None:
+    def __init__(self, require_mask: bool = True) -> None:
+        self.require_mask = require_mask     # False only to decode server -> client frames
         self.buf = bytearray()
         self.frag_op: Optional[int] = None
         self.frag: List[bytes] = []
+        self.frag_len = 0
 
     def feed(self, data: bytes) -> List[Tuple[int, bytes]]:
         self.buf += data
@@ -70,6 +77,10 @@ class FrameParser:
                 pos = 10
             if n > MAX_MESSAGE:
                 raise ValueError("frame too large")
+            if not masked and self.require_mask:
+                raise ValueError("unmasked client frame")
+            if op >= 0x8 and (not fin or n > 125):
+                raise ValueError("bad control frame")
             mask = b""
             if masked:
                 if len(self.buf) < pos + 4:
@@ -88,15 +99,20 @@ class FrameParser:
             if op == 0x0:                      # continuation
                 if self.frag_op is None:
                     raise ValueError("unexpected continuation")
+                self.frag_len += len(payload)
+                if self.frag_len > MAX_MESSAGE:
+                    raise ValueError("message too large")
                 self.frag.append(payload)
                 if fin:
                     out.append((self.frag_op, b"".join(self.frag)))
-                    self.frag_op, self.frag = None, []
+                    self.frag_op, self.frag, self.frag_len = None, [], 0
                 continue
+            if self.frag_op is not None:
+                raise ValueError("new data frame inside a fragmented message")
             if fin:
                 out.append((op, payload))
             else:
-                self.frag_op, self.frag = op, [payload]
+                self.frag_op, self.frag, self.frag_len = op, [payload], len(payload)
 
 
 class RFC6455Protocol(asyncio.Protocol):
@@ -114,7 +130,9 @@ class RFC6455Protocol(asyncio.Protocol):
         self.accepted = False
         self.closed = False
         self.parser = FrameParser()
+        # bounded: the /clock handler never reads; a flooding client is paused, then failed
         self.queue: "asyncio.Queue[Dict[str, Any]]" = asyncio.Queue()
+        self.reading_paused = False
         self.scope: Dict[str, Any] = {}
         self.key = b""
         self.task: Optional[asyncio.Task] = None
@@ -140,6 +158,11 @@ class RFC6455Protocol(asyncio.Protocol):
             self.head += data
             end = self.head.find(b"\r\n\r\n")
             if end < 0:
+                if len(self.head) > MAX_HANDSHAKE:
+                    self._reject(431)
+                return
+            if end > MAX_HANDSHAKE:
+                self._reject(431)
                 return
             rest = bytes(self.head[end + 4:])
             self._start(bytes(self.head[:end]))
@@ -152,6 +175,9 @@ class RFC6455Protocol(asyncio.Protocol):
             self._fail(1002)
             return
         for op, payload in msgs:
+            if op in (0x1, 0x2) and self._data_queued() >= MAX_QUEUED:
+                self._fail(1008)               # policy violation: the app is not reading
+                return
             if op == 0x1:
                 self.queue.put_nowait({"type": "websocket.receive", "text": payload.decode("utf-8", "replace")})
             elif op == 0x2:
@@ -210,7 +236,12 @@ class RFC6455Protocol(asyncio.Protocol):
                 self.transport.close()
 
     async def _receive(self) -> Dict[str, Any]:
-        return await self.queue.get()
+        msg = await self.queue.get()
+        if self.reading_paused and self.queue.qsize() < MAX_QUEUED // 4 and self.transport is not None \
+                and not self.transport.is_closing():
+            self.transport.resume_reading()
+            self.reading_paused = False
+        return msg
 
     async def _send(self, message: Dict[str, Any]) -> None:
         t = message["type"]
@@ -243,13 +274,21 @@ class RFC6455Protocol(asyncio.Protocol):
             self.transport.close()
 
     # ------------------------------------------------------------------ helpers
+    def _data_queued(self) -> int:
+        n = self.queue.qsize()
+        if n >= MAX_QUEUED // 2 and not self.reading_paused and self.transport is not None:
+            self.transport.pause_reading()     # back-pressure first; resumed as the app reads
+            self.reading_paused = True
+        return n
+
     def _write_frame(self, op: int, payload: bytes) -> None:
         if self.transport is not None and not self.transport.is_closing():
             self.transport.write(encode_frame(op, payload))
 
     def _reject(self, status: int) -> None:
         if self.transport is not None and not self.transport.is_closing():
-            self.transport.write(f"HTTP/1.1 {status} Forbidden\r\ncontent-length: 0\r\nconnection: close\r\n\r\n".encode())
+            reason = {403: "Forbidden", 431: "Request Header Fields Too Large", 500: "Internal Server Error"}.get(status, "Error")
+            self.transport.write(f"HTTP/1.1 {status} {reason}\r\ncontent-length: 0\r\nconnection: close\r\n\r\n".encode())
             self.closed = True
             self.transport.close()
 

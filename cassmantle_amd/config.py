@@ -80,14 +80,20 @@ class ModelConfig:
     steps: int = 50
     guidance_scale: float = 7.5
     scheduler: str = "pndm"               # pndm | ddim | euler
-    images_per_room: int = 1
-    dtype: str = "bf16"
+    # rooms that share one device pipeline have their concurrent generation requests batched
+    # into one denoise loop (game/content.BatchingImageGenerator): up to gen_batch_max images,
+    # collected for gen_batch_window_ms
+    gen_batch_max: int = 4
+    gen_batch_window_ms: float = 50.0
+    dtype: str = "bf16"                   # bf16 (HIP kernels) | fp32 (CPU reference path only)
     device: str = "auto"                  # auto | cpu | cuda
+    gpu_blur: bool = True                 # /fetch/contents blur on the GPU (HIP kernel) when present
     use_graphs: bool = True               # hipGraph-captured denoise loop
     fp8_attention: bool = False           # BASELINE config 4 (SDXL)
-    weights_path: Optional[str] = None    # optional safetensors checkpoint dir
+    weights_path: Optional[str] = None    # diffusers-layout dir (unet/ vae/ text_encoder[_2]/ *.safetensors)
     seed: int = 0
     scorer: str = "minilm"               # minilm | wordvec
+    scorer_weights: Optional[str] = None  # BertModel / sentence-transformers MiniLM safetensors
     scorer_batch_window_ms: float = 1.0   # micro-batch window for streaming guess scoring
     prompt_generator: str = "synthetic"   # synthetic | lm | remote
     lm_model: str = "tiny-lm"             # tiny-lm | mistral-7b (models/lm.py)

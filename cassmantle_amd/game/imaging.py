@@ -71,6 +71,10 @@ class BlurCache:
         self.hits = 0
         self.misses = 0
 
+    def __len__(self) -> int:
+        with self._lock:
+            return len(self._lru)
+
     def get(self, version: str, jpeg: bytes, radius: float) -> bytes:
         r = quantize_radius(radius, self.bucket)
         key = (version, r)

@@ -350,15 +350,23 @@ class GameRoom:
     def fetch_story(self) -> Dict[str, str]:
         return self.store.hgetall(self.k("story"))
 
-    def fetch_masked_image(self, session: str) -> bytes:
-        """Blurred JPEG by the session's best score (``src/server.py:129-133``)."""
+    def masked_image_request(self, session: str) -> Optional[Tuple[str, bytes, float]]:
+        """The store reads of :meth:`fetch_masked_image` — (image version, JPEG, blur radius) —
+        done on the event loop so only the pure blur/encode work moves to a worker thread."""
         scores = self.fetch_client_scores(session)
         jpeg = self.store.hget(self.k("image"), "current")
         if jpeg is None:
-            return b""
+            return None
         version = self.store.hget(self.k("image"), "version") or self._version(jpeg)
         radius = score_to_blur(float(scores.get("max", self.cfg.min_score)), self.cfg.min_blur, self.cfg.max_blur)
-        return self.blur_cache.get(version, jpeg, radius)
+        return version, jpeg, radius
+
+    def render_masked_image(self, req: Optional[Tuple[str, bytes, float]]) -> bytes:
+        return b"" if req is None else self.blur_cache.get(*req)
+
+    def fetch_masked_image(self, session: str) -> bytes:
+        """Blurred JPEG by the session's best score (``src/server.py:129-133``)."""
+        return self.render_masked_image(self.masked_image_request(session))
 
     def reset_sessions(self) -> None:
         for s in self.store.smembers(self.k("sessions")):

@@ -9,16 +9,21 @@ The method names and return conventions follow Redis (``TTL`` returns -2 for a m
 -1 for no expiry) so the game logic reads like the reference's, but values are ``str`` (the
 reference decodes bytes everywhere) except for raw ``bytes`` payloads (JPEGs).
 
-Single event loop ⇒ no data races between coroutines on a single operation; multi-step
+Thread safety: the event loop is the main user, but worker threads (``asyncio.to_thread`` blur
+/ JPEG work, generation callbacks) touch it too, so every operation runs under one re-entrant
+mutex (expiry bookkeeping in ``_alive`` mutates the dicts even on reads).  Multi-step
 read-modify-write sequences that the reference leaves racy (``set_client_scores``,
-``src/server.py:79-82``) are made atomic with :meth:`StateStore.critical`.
+``src/server.py:79-82``) are made atomic across coroutines with :meth:`StateStore.critical`
+(SURVEY §5.2).
 """
 from __future__ import annotations
 
 import asyncio
-import contextlib
-import json
 import base64
+import contextlib
+import functools
+import json
+import threading
 import uuid
 from typing import Any, Dict, Iterable, Optional, Set, Union
 
@@ -39,8 +44,17 @@ def _enc(v: Any) -> Value:
     return str(v)
 
 
+def _synchronized(fn):
+    @functools.wraps(fn)
+    def wrapper(self, *a, **kw):
+        with self._mu:
+            return fn(self, *a, **kw)
+    return wrapper
+
+
 class StateStore:
     def __init__(self, clock: Optional[Clock] = None) -> None:
+        self._mu = threading.RLock()
         self.clock = clock or Clock()
         self._data: Dict[str, Any] = {}
         self._expiry: Dict[str, float] = {}
@@ -49,6 +63,7 @@ class StateStore:
         self.ops = 0  # operation counter (metrics)
 
     # ------------------------------------------------------------------ expiry
+    @_synchronized
     def _alive(self, key: str) -> bool:
         exp = self._expiry.get(key)
         if exp is not None and self.clock.now() >= exp:
@@ -57,6 +72,7 @@ class StateStore:
             return False
         return key in self._data
 
+    @_synchronized
     def _get(self, key: str, typ: type) -> Any:
         self.ops += 1
         if not self._alive(key):
@@ -67,10 +83,12 @@ class StateStore:
         return v
 
     # ------------------------------------------------------------------ keys
+    @_synchronized
     def exists(self, *keys: str) -> int:
         self.ops += 1
         return sum(1 for k in keys if k is not None and self._alive(k))
 
+    @_synchronized
     def delete(self, *keys: str) -> int:
         n = 0
         for k in keys:
@@ -80,12 +98,14 @@ class StateStore:
             self._expiry.pop(k, None)
         return n
 
+    @_synchronized
     def expire(self, key: str, seconds: float) -> bool:
         if not self._alive(key):
             return False
         self._expiry[key] = self.clock.now() + float(seconds)
         return True
 
+    @_synchronized
     def ttl(self, key: str) -> int:
         """Redis TTL: integer seconds remaining (rounded like Redis: ceil of ms/1000 rounded
         to nearest), -2 if missing, -1 if no expiry."""
@@ -98,6 +118,7 @@ class StateStore:
         rem = exp - self.clock.now()
         return int(rem + 0.5)
 
+    @_synchronized
     def pttl(self, key: str) -> float:
         if not self._alive(key):
             return -2
@@ -105,6 +126,7 @@ class StateStore:
         return -1 if exp is None else (exp - self.clock.now())
 
     # ------------------------------------------------------------------ strings
+    @_synchronized
     def set(self, key: str, value: Any, ex: Optional[float] = None, nx: bool = False) -> bool:
         if nx and self._alive(key):
             return False
@@ -115,13 +137,16 @@ class StateStore:
             self._expiry.pop(key, None)
         return True
 
+    @_synchronized
     def setex(self, key: str, seconds: float, value: Any) -> bool:
         return self.set(key, value, ex=seconds)
 
+    @_synchronized
     def get(self, key: str) -> Optional[Value]:
         return self._get(key, (str, bytes))
 
     # ------------------------------------------------------------------ hashes
+    @_synchronized
     def hset(self, key: str, field: Optional[str] = None, value: Any = None,
              mapping: Optional[Dict[str, Any]] = None) -> int:
         h = self._get(key, dict)
@@ -139,14 +164,17 @@ class StateStore:
             h[f] = _enc(v)
         return n
 
+    @_synchronized
     def hget(self, key: str, field: str) -> Optional[Value]:
         h = self._get(key, dict)
         return None if h is None else h.get(str(field))
 
+    @_synchronized
     def hgetall(self, key: str) -> Dict[str, Value]:
         h = self._get(key, dict)
         return {} if h is None else dict(h)
 
+    @_synchronized
     def hdel(self, key: str, *fields_: str) -> int:
         h = self._get(key, dict)
         if h is None:
@@ -159,6 +187,7 @@ class StateStore:
             self.delete(key)
         return n
 
+    @_synchronized
     def hincrby(self, key: str, field: str, amount: int = 1) -> int:
         h = self._get(key, dict)
         if h is None:
@@ -169,11 +198,13 @@ class StateStore:
         h[field] = str(cur)
         return cur
 
+    @_synchronized
     def hexists(self, key: str, field: str) -> bool:
         h = self._get(key, dict)
         return h is not None and str(field) in h
 
     # ------------------------------------------------------------------ sets
+    @_synchronized
     def sadd(self, key: str, *members: str) -> int:
         s = self._get(key, set)
         if s is None:
@@ -186,6 +217,7 @@ class StateStore:
                 n += 1
         return n
 
+    @_synchronized
     def srem(self, key: str, *members: str) -> int:
         s = self._get(key, set)
         if s is None:
@@ -197,14 +229,17 @@ class StateStore:
                 n += 1
         return n
 
+    @_synchronized
     def smembers(self, key: str) -> Set[str]:
         s = self._get(key, set)
         return set() if s is None else set(s)
 
+    @_synchronized
     def sismember(self, key: str, member: str) -> bool:
         s = self._get(key, set)
         return s is not None and member in s
 
+    @_synchronized
     def scard(self, key: str) -> int:
         s = self._get(key, set)
         return 0 if s is None else len(s)
@@ -239,6 +274,7 @@ class StateStore:
         return lk
 
     # ------------------------------------------------------------------ snapshot
+    @_synchronized
     def snapshot(self) -> Dict[str, Any]:
         """JSON-serialisable dump (checkpoint/resume).  TTLs are stored as
         remaining seconds so they survive a restart on a different clock."""
@@ -260,6 +296,7 @@ class StateStore:
             out[k] = enc
         return out
 
+    @_synchronized
     def restore(self, snap: Dict[str, Any]) -> None:
         self._data.clear()
         self._expiry.clear()

@@ -228,7 +228,7 @@ class LMTextGenerator:
         for t, v in zip((self.tok_buf, self.pos, self.lens, self.idx), saved):
             t.copy_(v)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with TRACER.capturing(), torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._step()
         for t, v in zip((self.tok_buf, self.pos, self.lens, self.idx), saved):
             t.copy_(v)

@@ -189,9 +189,9 @@ class MiniLMEncoder(nn.Module):
 
     def forward(self, ids: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
         """ids [B, T], lens [B] -> L2-normalised mean-pooled embeddings [B, D] fp32."""
-        B, T = ids.shape
-        x = self.word_embeddings[ids] + self.position_embeddings[:T][None] + self.token_type_embeddings[0]
-        x = self.emb_ln(x)
+        # gather + position + token-type-0 add + LayerNorm in one kernel
+        x = ops.embed_layer_norm(self.word_embeddings, ids, self.position_embeddings, self.token_type_embeddings[0],
+                                 self.emb_ln.weight, self.emb_ln.bias, self.emb_ln.eps)
         for blk in self.layers:
             x = blk(x, lens)
         return ops.mean_pool_l2(x, lens)

@@ -120,7 +120,12 @@ def export_diffusers(model: nn.Module, kind: str) -> Dict[str, torch.Tensor]:
 
 
 def load_state(model: nn.Module, sd: Dict[str, torch.Tensor], kind: str, strict: bool = True) -> List[str]:
-    """diffusers-named state dict -> our module (in place).  Returns missing names."""
+    """diffusers-named state dict -> our module (in place).  Returns missing names.  CLIP text
+    towers are accepted with or without the ``text_model.`` prefix (checkpoint files carry it,
+    a transformers>=5 ``CLIPTextModel.state_dict()`` does not)."""
+    if kind == "clip" and not any(k.startswith("text_model.") for k in sd):
+        sd = {("text_model." + k if k.startswith(("embeddings.", "encoder.", "final_layer_norm.")) else k): v
+              for k, v in sd.items()}
     own = model.state_dict()
     missing = []
     with torch.no_grad():
@@ -211,6 +216,64 @@ def export_causal_lm(model: nn.Module) -> Dict[str, torch.Tensor]:
     return {k: v.detach().cpu().contiguous() for k, v in out.items()}
 
 
+# ---------------------------------------------------------------- BERT / MiniLM (guess scorer)
+def _bert_pairs(model: nn.Module, prefix: str = "") -> List[Tuple[torch.Tensor, List[str]]]:
+    """(our tensor, HF BertModel source names) — several sources are concatenated (fused QKV)."""
+    p = prefix
+    out = [(model.word_embeddings, [p + "embeddings.word_embeddings.weight"]),
+           (model.position_embeddings, [p + "embeddings.position_embeddings.weight"]),
+           (model.token_type_embeddings, [p + "embeddings.token_type_embeddings.weight"]),
+           (model.emb_ln.weight, [p + "embeddings.LayerNorm.weight"]),
+           (model.emb_ln.bias, [p + "embeddings.LayerNorm.bias"])]
+    for i, blk in enumerate(model.layers):
+        e = f"{p}encoder.layer.{i}."
+        for kind in ("weight", "bias"):
+            out.append((getattr(blk.attention.to_qkv, kind),
+                        [e + f"attention.self.{n}.{kind}" for n in ("query", "key", "value")]))
+            out.append((getattr(blk.attention.to_out, kind), [e + f"attention.output.dense.{kind}"]))
+            out.append((getattr(blk.attention_ln, kind), [e + f"attention.output.LayerNorm.{kind}"]))
+            out.append((getattr(blk.intermediate, kind), [e + f"intermediate.dense.{kind}"]))
+            out.append((getattr(blk.output, kind), [e + f"output.dense.{kind}"]))
+            out.append((getattr(blk.output_ln, kind), [e + f"output.LayerNorm.{kind}"]))
+    return out
+
+
+def load_bert(model: nn.Module, sd: Dict[str, torch.Tensor]) -> List[str]:
+    """transformers ``BertModel`` / sentence-transformers MiniLM state dict -> our
+    :class:`~cassmantle_amd.models.text.MiniLMEncoder` (query/key/value fused into ``to_qkv``).
+    Accepts the bare, ``bert.`` and ``0.auto_model.`` key prefixes.  Returns missing names."""
+    prefix = ""
+    for cand in ("", "bert.", "0.auto_model.", "model."):
+        if cand + "embeddings.word_embeddings.weight" in sd:
+            prefix = cand
+            break
+    missing: List[str] = []
+    with torch.no_grad():
+        for dst, names in _bert_pairs(model, prefix):
+            parts = [sd.get(n) for n in names]
+            if any(t is None for t in parts):
+                missing.extend(n for n, t in zip(names, parts) if t is None)
+                continue
+            t = parts[0] if len(parts) == 1 else torch.cat(parts, 0)
+            if dst.shape[0] > t.shape[0] and dst.dim() == 2 and dst.shape[1] == t.shape[1] and "position" in names[0]:
+                dst[: t.shape[0]].copy_(t.to(dst.dtype))       # shorter position table
+                continue
+            if tuple(t.shape) != tuple(dst.shape):
+                raise ValueError(f"{names[0]}: checkpoint {tuple(t.shape)} vs model {tuple(dst.shape)}")
+            dst.copy_(t.to(dst.dtype))
+    return missing
+
+
+def export_bert(model: nn.Module) -> Dict[str, torch.Tensor]:
+    """Inverse of :func:`load_bert` (HF ``BertModel`` names, split Q/K/V)."""
+    out: Dict[str, torch.Tensor] = {}
+    for src, names in _bert_pairs(model):
+        t = src.detach().cpu()
+        for n, part in zip(names, t.chunk(len(names), 0)):
+            out[n] = part.contiguous()
+    return out
+
+
 def read_safetensors(path: str) -> Dict[str, torch.Tensor]:
     from safetensors.torch import load_file
     if os.path.isdir(path):
@@ -223,7 +286,12 @@ def read_safetensors(path: str) -> Dict[str, torch.Tensor]:
 
 
 def load_pipeline_weights(sd_pipe, root: str) -> Dict[str, int]:
-    """Load a diffusers-layout directory into a :class:`~cassmantle_amd.pipeline.StableDiffusion`."""
+    """Load a diffusers-layout directory into a :class:`~cassmantle_amd.pipeline.StableDiffusion`.
+    Returns the number of missing tensors per component found; raises if the directory holds
+    none of ``unet/``, ``vae/``, ``text_encoder/`` (a wrong path must not silently keep random
+    weights)."""
+    if not any(os.path.exists(os.path.join(root, sub)) for sub in ("unet", "vae", "text_encoder")):
+        raise FileNotFoundError(f"{root}: no unet/, vae/ or text_encoder/ safetensors directory")
     stats = {}
     for sub, model, kind in (("unet", sd_pipe.unet, "unet"), ("vae", sd_pipe.vae, "vae"),
                              ("text_encoder", sd_pipe.text_encoders[0], "clip")):

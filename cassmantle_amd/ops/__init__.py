@@ -405,6 +405,21 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
+def embed_layer_norm(word: torch.Tensor, ids: torch.Tensor, pos: torch.Tensor, add: Optional[torch.Tensor],
+                     weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float) -> torch.Tensor:
+    """Encoder input layer in one kernel: LN(word[ids] + pos[t] + add) for ids [B, T] ->
+    [B, T, D] (gather + two adds + LayerNorm; BERT/MiniLM token-type-0 embedding as ``add``)."""
+    B, T = ids.shape
+    if not _use_hip(word):
+        x = word[ids] + pos[:T][None]
+        if add is not None:
+            x = x + add
+        return layer_norm(x, weight, bias, eps)
+    out = torch.empty((B, T, word.shape[-1]), device=word.device, dtype=word.dtype)
+    ext().embed_layer_norm(word, ids.contiguous().view(-1), pos, T, add, weight, bias, out, float(eps))
+    return out
+
+
 def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     if not _use_hip(x):
         return ref.rms_norm(x, weight, eps)

@@ -335,6 +335,22 @@ void layer_norm(const at::Tensor& x, const at::Tensor& gamma, const c10::optiona
   launch_layer_norm(bptr(x), bptr(gamma), opt_bptr(beta), bptr_mut(out), x.numel() / D, D, (float)eps, cur_stream());
 }
 
+// encoder input layer: out[r] = LN(word[ids[r]] + pos[r % seq] + add); ids int64 [rows]
+void embed_layer_norm(const at::Tensor& word, const at::Tensor& ids, const at::Tensor& pos, int64_t seq,
+                      const c10::optional<at::Tensor>& add, const at::Tensor& gamma,
+                      const c10::optional<at::Tensor>& beta, at::Tensor& out, double eps) {
+  CHECK_DEV(word); CHECK_BF16(word); CHECK_CONTIG(word); CHECK_DEV(ids); CHECK_CONTIG(ids);
+  CHECK_BF16(pos); CHECK_CONTIG(pos); CHECK_BF16(gamma); CHECK_BF16(out); CHECK_CONTIG(out);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "embed_layer_norm: int64 ids");
+  const int D = (int)word.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 4096 && pos.size(-1) == D && out.numel() == ids.numel() * D,
+              "embed_layer_norm: D % 8 == 0, D <= 4096, out [rows, D]");
+  TORCH_CHECK(seq > 0 && pos.size(0) >= seq, "embed_layer_norm: position table shorter than seq");
+  launch_embed_layer_norm(bptr(word), reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()), bptr(pos), (int)seq,
+                          opt_bptr(add), bptr(gamma), opt_bptr(beta), bptr_mut(out), ids.numel(), D, (float)eps,
+                          cur_stream());
+}
+
 void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, double scale,
                int64_t causal, const c10::optional<at::Tensor>& kv_lens, int64_t fp8) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
@@ -414,9 +430,13 @@ void gaussian_blur(const at::Tensor& img, const at::Tensor& w, at::Tensor& out) 
   }
   auto wf = w.to(at::kFloat).contiguous();
   int R = (int)(wf.numel() - 1) / 2;
-  auto tmp = at::empty({img.numel()}, img.options().dtype(at::kFloat));
-  launch_gaussian_blur(img.data_ptr(), u8, (int)img.size(0), (int)img.size(1), (int)img.size(2), wf.data_ptr<float>(),
-                       R, tmp.data_ptr<float>(), out.data_ptr(), cur_stream());
+  const int C = (int)img.size(2);
+  // the LDS-tiled uint8 kernel (R <= 48, C in {1,3,4}) needs no global scratch
+  const bool tiled = u8 && R <= 48 && (C == 1 || C == 3 || C == 4);
+  at::Tensor tmp;
+  if (!tiled) tmp = at::empty({img.numel()}, img.options().dtype(at::kFloat));
+  launch_gaussian_blur(img.data_ptr(), u8, (int)img.size(0), (int)img.size(1), C, wf.data_ptr<float>(), R,
+                       tiled ? nullptr : tmp.data_ptr<float>(), out.data_ptr(), cur_stream());
 }
 
 void to_uint8(const at::Tensor& x, at::Tensor& out) {
@@ -540,6 +560,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bmm_nt", &bmm_nt);
   m.def("group_norm", &group_norm);
   m.def("layer_norm", &layer_norm);
+  m.def("embed_layer_norm", &embed_layer_norm);
   m.def("group_norm_stats", &group_norm_stats);
   m.def("channel_stats", &channel_stats);
   m.def("attention", &attention);

@@ -98,6 +98,10 @@ void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        long long rows, int D, float eps, hipStream_t s);
 // per-row (mean, rstd) float2 of [rows][D] (LayerNorm statistics for a folded-LN GEMM)
 void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s);
+// fused encoder input layer: y[r] = LN(word[ids[r]] + pos[r % seq] + add) (bf16, D % 8 == 0)
+void launch_embed_layer_norm(const uint16_t* word, const long long* ids, const uint16_t* pos, int seq,
+                             const uint16_t* add, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                             long long rows, int D, float eps, hipStream_t s);
 void launch_rms_norm(const uint16_t* x, const uint16_t* gamma, uint16_t* y, long long rows, int D, float eps,
                      hipStream_t s);
 

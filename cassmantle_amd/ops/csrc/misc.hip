@@ -6,8 +6,10 @@
 // * pair_cosine: row-wise cosine of two embedding matrices (MiniLM scorer).
 // * cosine_gemv (K15): table . v / (|row| |v|) for most_similar, one wave per row.
 // * mean_pool_l2 (K16 tail): masked mean over tokens + L2 normalisation, one block per row.
-// * gaussian_blur (K17): separable blur, horizontal pass -> f32 scratch -> vertical pass,
-//   edge clamp, uint8 or f32 images.
+// * gaussian_blur (K17): uint8 images (the served JPEG content), radius <= 48: ONE LDS-tiled
+//   kernel per 32x32 output tile — the clamped input tile + halo is staged in LDS once, the
+//   horizontal pass writes an f32 LDS intermediate, the vertical pass reads it (no global
+//   scratch, one launch).  Other inputs: separable two-pass with a global f32 scratch.
 // * to_uint8 (K18): VAE output [-1, 1] -> uint8 (x/2 + 0.5 clamp, *255, round).
 // * timestep_embedding (K10), latent_step (K11: CFG combine + scheduler update + next UNet
 //   input, reading its coefficient row through a device step counter so a hipGraph replays
@@ -247,9 +249,90 @@ void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, 
   hipLaunchKernelGGL(mean_pool_l2_kernel, dim3(B), dim3(256), (D + 64) * sizeof(float), s, h, lens, out, T, D);
 }
 
+constexpr int BLUR_TS = 32;
+constexpr int BLUR_MAXR = 48;
+
+CM_DEVICE int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+template <int C>
+__global__ void __launch_bounds__(256) blur_tile_kernel(const uint8_t* __restrict__ img, int H, int W,
+                                                        const float* __restrict__ w, int R, uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char blur_sm[];
+  const int E = BLUR_TS + 2 * R;                               // staged tile edge (with halo)
+  uint8_t* tin = blur_sm;                                      // [E][E][C] u8
+  float* mid = reinterpret_cast<float*>(blur_sm + ((E * E * C + 15) & ~15));   // [E][TS][C]
+  float* ws = mid + E * BLUR_TS * C;                           // [2R+1]
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * BLUR_TS - R, y0 = blockIdx.y * BLUR_TS - R;
+  for (int i = tid; i < 2 * R + 1; i += 256) ws[i] = w[i];
+  for (int i = tid; i < E * E; i += 256) {
+    const int r = i / E, c = i - r * E;
+    const int gy = clampi(y0 + r, 0, H - 1), gx = clampi(x0 + c, 0, W - 1);   // edge clamp
+    const uint8_t* src = img + ((long long)gy * W + gx) * C;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) tin[i * C + ch] = src[ch];
+  }
+  __syncthreads();
+  for (int i = tid; i < E * BLUR_TS; i += 256) {              // horizontal pass -> LDS f32
+    const int r = i / BLUR_TS, j = i - r * BLUR_TS;
+    float acc[C];
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) acc[ch] = 0.f;
+    const uint8_t* row = tin + (r * E + j) * C;
+    for (int k = 0; k <= 2 * R; ++k) {
+      const float wk = ws[k];
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) acc[ch] = fmaf(wk, (float)row[k * C + ch], acc[ch]);
+    }
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) mid[i * C + ch] = acc[ch];
+  }
+  __syncthreads();
+  for (int i = tid; i < BLUR_TS * BLUR_TS; i += 256) {        // vertical pass -> uint8
+    const int r = i / BLUR_TS, j = i - r * BLUR_TS;
+    const int gy = blockIdx.y * BLUR_TS + r, gx = blockIdx.x * BLUR_TS + j;
+    if (gy >= H || gx >= W) continue;
+    float acc[C];
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) acc[ch] = 0.f;
+    for (int k = 0; k <= 2 * R; ++k) {
+      const float wk = ws[k];
+      const float* m = mid + ((r + k) * BLUR_TS + j) * C;
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) acc[ch] = fmaf(wk, m[ch], acc[ch]);
+    }
+    uint8_t* dst = out + ((long long)gy * W + gx) * C;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) dst[ch] = (uint8_t)fminf(fmaxf(rintf(acc[ch]), 0.f), 255.f);
+  }
+}
+
+template <int C>
+void launch_blur_tile(const uint8_t* img, int H, int W, const float* w, int R, uint8_t* out, hipStream_t s) {
+  const int E = BLUR_TS + 2 * R;
+  const size_t lds = ((size_t)(E * E * C + 15) & ~(size_t)15) + sizeof(float) * ((size_t)E * BLUR_TS * C + 2 * R + 1);
+  static bool once = false;
+  if (!once) {    // up to ~99 KiB at R = 48 (first call happens outside any graph capture)
+    (void)hipFuncSetAttribute((const void*)&blur_tile_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(((size_t)(BLUR_TS + 2 * BLUR_MAXR) * (BLUR_TS + 2 * BLUR_MAXR) * C + 15 & ~(size_t)15) +
+                                    sizeof(float) * ((size_t)(BLUR_TS + 2 * BLUR_MAXR) * BLUR_TS * C + 2 * BLUR_MAXR + 1)));
+    once = true;
+  }
+  dim3 grid((W + BLUR_TS - 1) / BLUR_TS, (H + BLUR_TS - 1) / BLUR_TS);
+  hipLaunchKernelGGL(blur_tile_kernel<C>, grid, dim3(256), lds, s, img, H, W, w, R, out);
+}
+
 void launch_gaussian_blur(const void* img, int u8, int H, int W, int C, const float* w, int R, float* tmp,
                           void* out, hipStream_t s) {
   long long n = (long long)H * W * C;
+  if (u8 && R <= BLUR_MAXR && (C == 1 || C == 3 || C == 4)) {
+    const uint8_t* im = reinterpret_cast<const uint8_t*>(img);
+    uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    if (C == 3) launch_blur_tile<3>(im, H, W, w, R, o, s);
+    else if (C == 4) launch_blur_tile<4>(im, H, W, w, R, o, s);
+    else launch_blur_tile<1>(im, H, W, w, R, o, s);
+    return;
+  }
   if (u8) {
     hipLaunchKernelGGL(blur_h_kernel<true>, dim3(nblk(n, 256)), dim3(256), 0, s, img, H, W, C, w, R, tmp);
     hipLaunchKernelGGL(blur_v_kernel<true>, dim3(nblk(n, 256)), dim3(256), 0, s, tmp, H, W, C, w, R, out);

@@ -374,17 +374,29 @@ __global__ void __launch_bounds__(GN_THREADS) channel_stats_kernel(const uint16_
 // LayerNorm / RMSNorm (RMS: no mean subtraction, no beta): T lanes per row, VPL vectors per lane
 // STATS: write only the row (mean, rstd) as float2 into y (LayerNorm folded into the next GEMM,
 // whose epilogue applies them: no normalised copy of the activation is written or re-read)
-template <int VPL, bool RMS, bool STATS = false>
+// EMB: the row is the token-embedding sum of an encoder's input layer, gathered here instead of
+// read from x: word[ids[row]] + pos[row % seq] + add (MiniLM / BERT: word + position + token
+// type 0), so the scorer's embedding step is ONE kernel (gather + add + LayerNorm) instead of
+// three ATen index/add launches plus the LayerNorm.
+struct EmbArgs {
+  const long long* ids = nullptr;     // [rows] token ids
+  const uint16_t* pos = nullptr;      // [>= seq][D]
+  const uint16_t* add = nullptr;      // [D] (nullable)
+  int seq = 1;
+};
+
+template <int VPL, bool RMS, bool STATS = false, bool EMB = false>
 __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gamma,
                           const uint16_t* __restrict__ beta, uint16_t* __restrict__ y,
-                          long long rows, int D, int T, float eps) {
+                          long long rows, int D, int T, float eps, EmbArgs e = EmbArgs()) {
   const int lane = threadIdx.x & 63;
   const int seg = lane / T, sl = lane - seg * T;
   const int rows_per_wave = 64 / T;
   const long long row = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * rows_per_wave + seg;
   const bool ok = row < rows;
   const int V = D / 8;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + (ok ? row : 0) * D);
+  const long long src_row = EMB ? (ok ? e.ids[row] : 0) : (ok ? row : 0);
+  const uint4* xr = reinterpret_cast<const uint4*>(x + src_row * D);
   float f[VPL][8];
   float s = 0.f;
 #pragma unroll
@@ -392,6 +404,17 @@ __global__ void ln_kernel(const uint16_t* __restrict__ x, const uint16_t* __rest
     const int v = sl + T * j;
     if (ok && v < V) {
       unpack8(xr[v], f[j]);
+      if constexpr (EMB) {
+        float a[8];
+        unpack8(reinterpret_cast<const uint4*>(e.pos + (row % e.seq) * D)[v], a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[j][k] = bf2f(f2bf(f[j][k] + a[k]));   // bf16 adds, as the
+        if (e.add) {                                                         // eager model rounds
+          unpack8(reinterpret_cast<const uint4*>(e.add)[v], a);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[j][k] = bf2f(f2bf(f[j][k] + a[k]));
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += f[j][k];
     } else {
@@ -513,31 +536,39 @@ void launch_channel_stats(const uint16_t* x, long long* stats, int B, long long 
                        rpc);
 }
 
-template <int VPL, bool RMS, bool STATS>
+template <int VPL, bool RMS, bool STATS, bool EMB>
 static void launch_ln_t(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
-                        long long rows, int D, int T, float eps, hipStream_t s) {
+                        long long rows, int D, int T, float eps, const EmbArgs& e, hipStream_t s) {
   const long long rows_per_block = 4LL * (64 / T);
   dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block));
-  hipLaunchKernelGGL((ln_kernel<VPL, RMS, STATS>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, T, eps);
+  hipLaunchKernelGGL((ln_kernel<VPL, RMS, STATS, EMB>), grid, dim3(256), 0, s, x, gamma, beta, y, rows, D, T, eps, e);
 }
 
-template <bool RMS, bool STATS = false>
+template <bool RMS, bool STATS = false, bool EMB = false>
 static void launch_ln(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
-                      long long rows, int D, float eps, hipStream_t s) {
+                      long long rows, int D, float eps, hipStream_t s, const EmbArgs& e = EmbArgs()) {
   const int V = D / 8;
   int T = 1;
   while (T < 64 && T * 8 < V) T <<= 1;                 // VPL <= 8 (D <= 4096)
   const int VPL = (V + T - 1) / T;
   switch (VPL) {
-    case 1: launch_ln_t<1, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 2: launch_ln_t<2, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 3: launch_ln_t<3, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 4: launch_ln_t<4, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 5: launch_ln_t<5, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 6: launch_ln_t<6, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    case 7: launch_ln_t<7, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
-    default: launch_ln_t<8, RMS, STATS>(x, gamma, beta, y, rows, D, T, eps, s); break;
+    case 1: launch_ln_t<1, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 2: launch_ln_t<2, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 3: launch_ln_t<3, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 4: launch_ln_t<4, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 5: launch_ln_t<5, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 6: launch_ln_t<6, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    case 7: launch_ln_t<7, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
+    default: launch_ln_t<8, RMS, STATS, EMB>(x, gamma, beta, y, rows, D, T, eps, e, s); break;
   }
+}
+
+void launch_embed_layer_norm(const uint16_t* word, const long long* ids, const uint16_t* pos, int seq,
+                             const uint16_t* add, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
+                             long long rows, int D, float eps, hipStream_t s) {
+  EmbArgs e;
+  e.ids = ids; e.pos = pos; e.add = add; e.seq = seq;
+  launch_ln<false, false, true>(word, gamma, beta, y, rows, D, eps, s, e);
 }
 
 void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s) {

@@ -29,7 +29,7 @@ from .models.schedulers import SchedulePlan, make_plan
 from .models.text import CLIP_BIGG, CLIP_L, TINY_CLIP, CLIPTextEncoder, CLIPTextConfig
 from .models.unet import SD15_UNET, SDXL_UNET, TINY_UNET, UNet, UNetConfig
 from .models.vae import SD_VAE, SDXL_VAE, TINY_VAE, VAEConfig, VAEDecoder
-from .utils.tracing import span
+from .utils.tracing import TRACER, span
 
 
 @dataclass
@@ -179,7 +179,10 @@ class StableDiffusion:
                 self._unet_step(st)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local capture mode: other threads (the scorer's stream, a metrics scrape) may
+        # keep making CUDA calls while this thread captures; the tracer also defers its event
+        # queries for the duration
+        with TRACER.capturing(), torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._unet_step(st)
         st.graph = g
 
@@ -258,9 +261,15 @@ class DiffusionImageGenerator(ImageGenerator):
 
     def __init__(self, model: str = "sd15", device=None, steps: Optional[int] = None,
                  guidance: Optional[float] = None, scheduler: Optional[str] = None,
-                 use_graphs: bool = True, fp8_attention: bool = False, seed: int = 0) -> None:
+                 use_graphs: bool = True, fp8_attention: bool = False, seed: int = 0,
+                 dtype=torch.bfloat16, weights_path: Optional[str] = None) -> None:
         self.sd = StableDiffusion(SPECS[model], device=device, use_graphs=use_graphs,
-                                  fp8_attention=fp8_attention, seed=seed)
+                                  fp8_attention=fp8_attention, seed=seed, dtype=dtype)
+        self.weights_loaded: Optional[Dict[str, int]] = None
+        if weights_path:
+            # diffusers-layout checkpoint (ModelConfig.weights_path); random init otherwise
+            from .models.weights import load_pipeline_weights
+            self.weights_loaded = load_pipeline_weights(self.sd, weights_path)
         self.resolution = self.sd.spec.resolution
         self.kw = dict(steps=steps, guidance=guidance, scheduler=scheduler)
 

@@ -13,9 +13,23 @@ from typing import Callable, Optional
 import torch
 
 from ..config import Config
-from ..game.content import ImageGenerator, SolidImageGenerator
+from ..game.content import BatchingImageGenerator, ImageGenerator, SolidImageGenerator
 from ..game.service import GameService
 from ..scoring.batcher import BatchingScorer
+
+
+_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32}
+
+
+def model_dtype(cfg: Config, device: str) -> torch.dtype:
+    """``ModelConfig.dtype``: the HIP kernels are bf16-only; fp32 selects the CPU reference path
+    (tests / parity) and is rejected on a GPU rather than silently ignored."""
+    dt = _DTYPES.get(cfg.model.dtype.lower())
+    if dt is None:
+        raise ValueError(f"dtype={cfg.model.dtype!r}: expected bf16 or fp32")
+    if dt != torch.bfloat16 and str(device).startswith("cuda"):
+        raise ValueError("dtype=fp32 runs only on the CPU reference path; the GPU kernels are bf16")
+    return dt
 
 
 def build_scorer(cfg: Config, device: Optional[str] = None):
@@ -26,8 +40,31 @@ def build_scorer(cfg: Config, device: Optional[str] = None):
     else:
         from ..scoring.encoder import EncoderBackend
         # high-priority stream: guess scoring is dispatched ahead of queued denoise kernels
-        backend = EncoderBackend(device=dev, stream_priority=-1 if dev.startswith("cuda") else None)
+        backend = EncoderBackend(device=dev, stream_priority=-1 if dev.startswith("cuda") else None,
+                                 dtype=model_dtype(cfg, dev))
+        if cfg.model.scorer_weights:
+            from ..models.weights import load_bert, read_safetensors
+            missing = load_bert(backend.model, read_safetensors(cfg.model.scorer_weights))
+            if missing:
+                raise KeyError(f"scorer_weights: {len(missing)} tensors missing, e.g. {missing[:3]}")
     return BatchingScorer(backend, cfg.game.min_score, window_ms=cfg.model.scorer_batch_window_ms)
+
+
+def build_blur_fn(cfg: Config, device: Optional[str] = None):
+    """The /fetch/contents blur (``mask_image``, ``src/backend.py:322-324``) on the GPU: the HIP
+    LDS-tiled Gaussian (ops.gaussian_blur) on its own stream.  ``None`` -> PIL on the CPU."""
+    dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    if not cfg.model.gpu_blur or not dev.startswith("cuda"):
+        return None
+    from .. import ops
+    stream = torch.cuda.Stream(device=dev)
+
+    def blur(img, radius: float):
+        with torch.cuda.stream(stream):
+            x = torch.from_numpy(img).to(dev, non_blocking=False)
+            y = ops.gaussian_blur(x, radius)
+            return y.cpu().numpy()
+    return blur
 
 
 def build_prompt_generator(cfg: Config, device: Optional[str] = None):
@@ -66,17 +103,23 @@ def build_image_generator(cfg: Config, device: Optional[str] = None) -> ImageGen
     if m.image_model == "solid" or not use_gpu:
         return SolidImageGenerator(resolution=min(m.resolution, 256))
     from ..pipeline import DiffusionImageGenerator
-    return DiffusionImageGenerator(m.image_model, device=device or "cuda", steps=m.steps,
+    dev = device or "cuda"
+    return DiffusionImageGenerator(m.image_model, device=dev, steps=m.steps,
                                    guidance=m.guidance_scale, scheduler=m.scheduler,
-                                   use_graphs=m.use_graphs, fp8_attention=m.fp8_attention, seed=m.seed)
+                                   use_graphs=m.use_graphs, fp8_attention=m.fp8_attention, seed=m.seed,
+                                   dtype=model_dtype(cfg, dev), weights_path=m.weights_path)
 
 
 def build_service(cfg: Config, image_gen_for_room: Optional[Callable[[str], ImageGenerator]] = None,
                   **kw) -> GameService:
     scorer = build_scorer(cfg)
     if image_gen_for_room is None:
-        gen = build_image_generator(cfg)
-        image_gen_for_room = lambda rid: gen  # noqa: E731 - one device pipeline shared by rooms
+        # one device pipeline shared by every room: requests are serialised and batched
+        gen = BatchingImageGenerator(build_image_generator(cfg), max_batch=cfg.model.gen_batch_max,
+                                     window_s=cfg.model.gen_batch_window_ms / 1e3 if cfg.game.num_rooms > 1 else 0.0)
+        image_gen_for_room = lambda rid: gen  # noqa: E731
     if "prompt_gen" not in kw:
         kw["prompt_gen"] = build_prompt_generator(cfg)
+    if "blur_fn" not in kw:
+        kw["blur_fn"] = build_blur_fn(cfg)
     return GameService(cfg, scorer, image_gen_for_room=image_gen_for_room, **kw)

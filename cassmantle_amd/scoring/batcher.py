@@ -9,10 +9,12 @@ coroutines.  Latencies are recorded for the p50/p99 metric (BASELINE config 1/5)
 """
 from __future__ import annotations
 
+import collections
+
 import asyncio
 import threading
 import time
-from typing import List, Optional, Sequence, Tuple
+from typing import Deque, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -25,7 +27,7 @@ class DirectScorer(Scorer):
     def __init__(self, backend: SimilarityBackend, min_score: float) -> None:
         self.backend = backend
         self.min_score = min_score
-        self.latencies: List[float] = []
+        self.latencies: Deque[float] = collections.deque(maxlen=4096)   # bounded window
 
     async def score(self, pairs):
         t0 = time.perf_counter()
@@ -49,7 +51,7 @@ class BatchingScorer(Scorer):
         self._queue: List[Tuple[Sequence[Tuple[str, str]], asyncio.Future, float]] = []
         self._flusher: Optional[asyncio.Task] = None
         self._lock = threading.Lock()  # one device batch at a time
-        self.latencies: List[float] = []
+        self.latencies: Deque[float] = collections.deque(maxlen=4096)   # bounded window
         self.batches = 0
         self.batched_pairs = 0
 

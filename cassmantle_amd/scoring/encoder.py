@@ -6,10 +6,15 @@ forward on the GPU (fused-op encoder, mean-pool + L2 in one kernel) and compared
 pair-cosine kernel.  Answer (secret-word) embeddings are cached for the round: a round has
 only ``num_masked`` secrets, so steady-state batches embed guesses only.
 
-BASELINE config 5 (live round: image generation and guess scoring on the same GPU): with
-``stream_priority`` the scorer runs on its own high-priority HIP stream, so its small launches
-are dispatched ahead of the queued denoise-graph kernels instead of behind them; the host sync
-for the result waits on that stream only.
+BASELINE config 5 (live round: image generation and guess scoring on the same GPU): the scorer
+always runs on its OWN non-blocking HIP stream (never the legacy default stream, which
+implicitly orders against other blocking work), high-priority with ``stream_priority=-1`` so its
+small launches are dispatched ahead of the queued denoise-graph kernels; the host sync for the
+result waits on that stream only.
+
+The encoder forward (~30 small launches: fused embedding+LN, 6 x {QKV GEMM, attention, out-proj,
+LN, FF GEMMs, LN}, mean-pool) is captured as a hipGraph per batch bucket (1, 2, 4, ... 256
+sequences, fixed 16 tokens) and replayed, so a micro-batch costs one graph launch.
 """
 from __future__ import annotations
 
@@ -25,23 +30,66 @@ from ..models.text import MINILM_L6, BertConfig, MiniLMEncoder
 
 
 class EncoderBackend(SimilarityBackend):
+    MAX_BUCKET = 256
+
     def __init__(self, cfg: BertConfig = MINILM_L6, device: str = "cpu", seed: int = 0,
-                 max_len: int = 16, dtype=torch.bfloat16, stream_priority: Optional[int] = None) -> None:
+                 max_len: int = 16, dtype=torch.bfloat16, stream_priority: Optional[int] = None,
+                 use_graphs: bool = True) -> None:
         self.device = torch.device(device)
         self.stream = None
-        if stream_priority is not None and self.device.type == "cuda":
-            self.stream = torch.cuda.Stream(device=self.device, priority=stream_priority)
+        if self.device.type == "cuda":
+            self.stream = torch.cuda.Stream(device=self.device, priority=stream_priority or 0)
         self.model = MiniLMEncoder(cfg, seed=seed, dtype=dtype, max_len=max_len).to(self.device).eval()
         self.max_len = max_len
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: Dict[int, tuple] = {}
         self._cache: Dict[str, torch.Tensor] = {}
+
+    def _capture(self, nb: int) -> tuple:
+        from ..utils.tracing import TRACER
+        tok = self.model.tokenizer
+        ids_h = torch.full((nb, self.max_len), tok.pad, dtype=torch.int64).pin_memory()
+        lens_h = torch.ones(nb, dtype=torch.int32).pin_memory()
+        ids = ids_h.to(self.device)
+        lens = lens_h.to(self.device)
+        self.model(ids, lens)                      # warm-up: allocator / first-launch work
+        torch.cuda.current_stream(self.device).synchronize()
+        g = torch.cuda.CUDAGraph()
+        with TRACER.capturing(), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            out = self.model(ids, lens)
+        entry = (g, ids_h, lens_h, ids, lens, out, torch.cuda.Event())
+        self._graphs[nb] = entry
+        return entry
 
     @torch.no_grad()
     def embed(self, texts: Sequence[str]) -> torch.Tensor:
-        # pad to a fixed length so shapes repeat (allocator reuse, graph-friendly)
-        return self.model.embed(list(texts), self.device, pad_to=self.max_len)
+        """L2-normalised embeddings [len(texts), D] fp32 (a fresh tensor, safe to keep).
+        Padded to a fixed token length so shapes repeat; on the GPU one graph replay per
+        micro-batch (batch padded to a power of two <= 256, larger batches in chunks)."""
+        texts = list(texts)
+        if not self.use_graphs:
+            return self.model.embed(texts, self.device, pad_to=self.max_len)
+        outs = []
+        for c0 in range(0, len(texts), self.MAX_BUCKET):
+            chunk = texts[c0:c0 + self.MAX_BUCKET]
+            n = len(chunk)
+            nb = 1 << max(0, (n - 1).bit_length())
+            entry = self._graphs.get(nb) or self._capture(nb)
+            g, ids_h, lens_h, ids, lens, out, copied = entry
+            tid, tl = self.model.tokenizer(chunk, pad_to=self.max_len)
+            copied.synchronize()                   # the pinned staging buffer is free again
+            ids_h[:n].copy_(tid)
+            lens_h[:n].copy_(tl)
+            ids.copy_(ids_h, non_blocking=True)
+            lens.copy_(lens_h, non_blocking=True)
+            copied.record()
+            g.replay()
+            outs.append(out[:n].clone())
+        return outs[0] if len(outs) == 1 else torch.cat(outs)
 
     def _ctx(self):
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
 
     @torch.no_grad()
     def similarity(self, guesses: Sequence[str], answers: Sequence[str]) -> np.ndarray:

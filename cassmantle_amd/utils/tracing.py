@@ -74,6 +74,7 @@ class Tracer:
         self._hist: Dict[str, Histogram] = {}
         self._pending: Deque[Tuple[str, object, object]] = deque()
         self._lock = threading.Lock()
+        self._capturing = 0
 
     # ---------------------------------------------------------------- recording
     def observe(self, stage: str, ms: float) -> None:
@@ -113,10 +114,26 @@ class Tracer:
                     self._pending.popleft()
             self.poll()
 
+    @contextlib.contextmanager
+    def capturing(self):
+        """Mark a hipGraph capture in progress: event queries from other threads (a /metrics
+        scrape on the event loop) are then deferred, since a query during a global-mode
+        capture is a prohibited call that can invalidate the capture."""
+        with self._lock:
+            self._capturing += 1
+        try:
+            yield
+        finally:
+            with self._lock:
+                self._capturing -= 1
+
     def poll(self) -> int:
-        """Resolve every completed GPU span (in order; stops at the first unfinished one)."""
+        """Resolve every completed GPU span (in order; stops at the first unfinished one).
+        A no-op while any graph capture is in progress (see :meth:`capturing`)."""
         done = []
         with self._lock:
+            if self._capturing:
+                return 0
             while self._pending:
                 stage, s, e = self._pending[0]
                 if not e.query():

@@ -131,3 +131,46 @@ def test_metrics_and_health():
     with client:
         assert client.get("/healthz").json()["ok"] is True
         assert "cassmantle_requests_total" in client.get("/metrics").text
+
+
+def test_cookieless_requests_get_a_session_cookie_not_orphans():
+    """a request without the cookie is served as a fresh session AND gets the cookie, so
+    repeated calls reuse it instead of piling up orphan session members"""
+    client, svc = make_client()
+    with client:
+        room = svc.room("")
+        r = client.get("/fetch/contents")
+        sid = r.cookies.get("session_id")
+        assert sid and room.session_exists(sid)
+        n = room.player_count()
+        for _ in range(3):                  # the client now sends the cookie
+            client.get("/fetch/contents")
+            client.post("/compute_score", json={"inputs": {}})
+        assert room.player_count() == n
+
+
+def test_round_boundary_prewarms_blur_cache_1024():
+    """end_round promotes the buffered 1024^2 image and precomputes every blur bucket off the
+    event loop; a page view at any score is then a cache hit (Appendix C.13 fix)"""
+    import asyncio
+    import time
+    cfg = Config()
+    cfg.game.rate_limit_enabled = False
+    cfg.game.blur_bucket = 1.0
+    backend = WordVectorBackend(vocab=["lantern", "tower"], vectors=np.eye(2, dtype=np.float32))
+    svc = GameService(cfg, BatchingScorer(backend, cfg.game.min_score),
+                      image_gen_for_room=lambda rid: SolidImageGenerator(1024), seed=0)
+    client = TestClient(create_app(svc, cfg, run_timers=False))
+    with client:
+        room = svc.room("")
+        client.portal.call(room.buffer_contents)
+        client.portal.call(room.end_round)
+        cache = room.blur_cache
+        deadline = time.time() + 60
+        while len(cache) < 16 and time.time() < deadline:     # 0..15 in 1.0 buckets
+            time.sleep(0.05)
+        assert cache.misses == 16 and len(cache) == 16
+        client.get("/init")
+        hits = cache.hits
+        img = base64.b64decode(client.get("/fetch/contents").json()["image"])
+        assert img[:2] == b"\xff\xd8" and cache.hits == hits + 1

@@ -453,3 +453,36 @@ def test_conv_up2_pp(cfg, force_cfg):
     out = ops.conv2d_up2(x, w, None, b)
     exp = ref.conv2d(x, w, b, 1, 1, None, True, None)
     assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("H,W,C,sigma", [(1024, 1024, 3, 15.0), (97, 130, 3, 0.6), (200, 75, 4, 9.3),
+                                         (64, 64, 1, 16.5), (50, 40, 3, 20.0)])
+def test_gaussian_blur_tiled(H, W, C, sigma):
+    """LDS-tiled blur (radius <= 48) and the two-pass fallback (sigma 20 -> radius 60) vs the fp32
+    separable reference with edge clamping; partial edge tiles included."""
+    img = (torch.rand(H, W, C, generator=torch.Generator().manual_seed(39)) * 255).to(torch.uint8).to(DEV)
+    out = ops.gaussian_blur(img, sigma)
+    exp = ref.gaussian_blur(img, sigma)
+    assert (out.int() - exp.int()).abs().max().item() <= 1
+
+
+def test_gpu_blur_fn_serves_blur_cache():
+    """the serving blur (runtime.factory.build_blur_fn) feeding the per-bucket JPEG cache,
+    prewarmed over every bucket of a 1024^2 image like a round boundary does"""
+    import numpy as np
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.game.imaging import BlurCache, encode_jpeg, decode_jpeg, blur_pil
+    from cassmantle_amd.runtime.factory import build_blur_fn
+    fn = build_blur_fn(Config(), "cuda")
+    assert fn is not None
+    rng = np.random.default_rng(0)
+    img = (rng.random((1024, 1024, 3)) * 255).astype(np.uint8)
+    g = fn(img, 7.5)
+    c = blur_pil(img, 7.5)
+    # PIL approximates the Gaussian with box blurs: close, not bit-equal
+    assert np.abs(g.astype(np.int32) - c.astype(np.int32)).mean() < 2.0
+    cache = BlurCache(blur_fn=fn, bucket=1.0)
+    jpeg = encode_jpeg(img)
+    assert cache.prewarm("v1", jpeg, 15.0) == 16
+    assert cache.misses == 16 and decode_jpeg(cache.get("v1", jpeg, 3.2)).shape == (1024, 1024, 3)
+    assert cache.hits >= 1

@@ -123,7 +123,15 @@ def test_euler_plan_sigmas():
 def test_checkpoint_roundtrip(kind, factory):
     a, b = factory(1), factory(2)
     sd = export_diffusers(a, kind)
-    assert all(t.dim() != 4 or t.shape[1] != t.shape[3] or True for t in sd.values())
+    # on disk every conv kernel is NCHW [Cout, Cin, kh, kw]: it must be exactly our
+    # [Cout, kh, kw, Cin] tensor permuted
+    own = a.state_dict()
+    convs = [n for n, t in own.items() if t.dim() == 4]
+    assert convs or kind == "clip"
+    for n in convs:
+        dn = next(k for k, t in sd.items() if t.dim() == 4 and t.shape == own[n].permute(0, 3, 1, 2).shape
+                  and torch.equal(t, own[n].permute(0, 3, 1, 2)))
+        assert dn
     if kind == "unet":
         assert any(k.startswith("down_blocks.0.attentions.0.transformer_blocks.0.attn1.to_q") for k in sd)
         assert sd["conv_in.weight"].shape[1] == 4            # NCHW on disk
@@ -169,3 +177,58 @@ def test_time_table_matches_per_step_time_embedding():
             ref = m(x, ts[e].expand(2), ctx, added)
             out = m(x, None, ctx, added, time_cond=(temb[e], tb[e]))
             assert torch.equal(out, ref)
+
+
+# ---------------------------------------------------------------- parity with transformers
+# Architecture AND checkpoint key mapping pinned against the public implementations (random
+# small configs, fp32 on the CPU reference path; the same ids go to both models).
+
+def test_minilm_matches_transformers_bert():
+    transformers = pytest.importorskip("transformers")
+    from cassmantle_amd.models.text import BertConfig as OurBert, MiniLMEncoder
+    from cassmantle_amd.models.weights import export_bert, load_bert
+    hf_cfg = transformers.BertConfig(vocab_size=500, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                                     intermediate_size=128, max_position_embeddings=64, hidden_act="gelu",
+                                     layer_norm_eps=1e-12, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    torch.manual_seed(0)
+    hf = transformers.BertModel(hf_cfg, add_pooling_layer=False).eval()
+    ours = MiniLMEncoder(OurBert(vocab_size=500, max_positions=64, dim=64, layers=2, heads=4, mlp=128),
+                         dtype=torch.float32).eval()
+    missing = load_bert(ours, hf.state_dict())
+    assert not missing
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(1, 500, (3, 12), generator=g)
+    lens = torch.tensor([12, 7, 3], dtype=torch.int32)
+    mask = (torch.arange(12)[None] < lens[:, None]).long()
+    ids = ids * mask
+    with torch.no_grad():
+        h = hf(input_ids=ids, attention_mask=mask).last_hidden_state
+        pooled = (h * mask[..., None]).sum(1) / mask.sum(1, keepdim=True)
+        ref = torch.nn.functional.normalize(pooled, dim=-1)
+        out = ours(ids, lens)
+    assert (out - ref).abs().max().item() < 1e-4
+    # the exporter is the inverse mapping
+    sd = export_bert(ours)
+    assert set(sd) <= set(hf.state_dict()) and all(torch.equal(sd[k], hf.state_dict()[k]) for k in sd)
+
+
+def test_clip_text_matches_transformers():
+    transformers = pytest.importorskip("transformers")
+    from cassmantle_amd.models.text import CLIPTextConfig as OurClip
+    hf_cfg = transformers.CLIPTextConfig(vocab_size=500, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                         num_attention_heads=4, max_position_embeddings=77, hidden_act="quick_gelu",
+                                         layer_norm_eps=1e-5, attention_dropout=0.0)
+    torch.manual_seed(0)
+    hf = transformers.CLIPTextModel(hf_cfg).eval()
+    ours = CLIPTextEncoder(OurClip(vocab_size=500, max_positions=77, dim=64, layers=2, heads=4, mlp=128,
+                                   act="quick_gelu"), dtype=torch.float32).eval()
+    missing = load_state(ours, hf.state_dict(), "clip", strict=False)
+    assert not missing, missing
+    ids = torch.randint(0, 500, (2, 77), generator=torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        ref = hf(input_ids=ids, output_hidden_states=True)
+        last, _ = ours(ids)
+        pen, _ = ours(ids, output_hidden=-2)
+    assert (last - ref.last_hidden_state).abs().max().item() < 1e-4
+    # SDXL conditions on the penultimate layer's hidden state (before the final LayerNorm)
+    assert (pen - ref.hidden_states[-2]).abs().max().item() < 1e-4

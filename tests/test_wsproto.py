@@ -75,7 +75,7 @@ def test_live_uvicorn_clock():
         head, _, rest = buf.partition(b"\r\n\r\n")
         assert head.startswith(b"HTTP/1.1 101")
         assert accept_key(key.encode()) in head
-        p = FrameParser()
+        p = FrameParser(require_mask=False)    # server frames are unmasked
         msgs = p.feed(rest)
         while not msgs:
             msgs = p.feed(c.recv(4096))
@@ -86,3 +86,92 @@ def test_live_uvicorn_clock():
     finally:
         server.should_exit = True
         th.join(timeout=10)
+
+
+def _unmasked(op, payload, fin=True):
+    b0 = (0x80 if fin else 0) | op
+    return bytes([b0, len(payload)]) + payload
+
+
+def test_parser_rejects_protocol_violations():
+    from cassmantle_amd.api import wsproto
+    with pytest.raises(ValueError):                      # RFC 6455 §5.1: clients must mask
+        FrameParser().feed(_unmasked(0x1, b"hi"))
+    with pytest.raises(ValueError):                      # fragmented control frame
+        FrameParser().feed(_mask(0x9, b"x", fin=False))
+    with pytest.raises(ValueError):                      # continuation without a start
+        FrameParser().feed(_mask(0x0, b"x"))
+    # reassembled message above the cap, although every single frame is small
+    p = FrameParser()
+    chunk = b"a" * 60000
+    p.feed(_mask(0x1, chunk, fin=False))
+    with pytest.raises(ValueError):
+        for _ in range(wsproto.MAX_MESSAGE // len(chunk) + 1):
+            p.feed(_mask(0x0, chunk, fin=False))
+
+
+class _FakeTransport:
+    def __init__(self):
+        self.written = b""
+        self.closed = False
+        self.paused = False
+
+    def write(self, b):
+        self.written += b
+
+    def close(self):
+        self.closed = True
+
+    def is_closing(self):
+        return self.closed
+
+    def pause_reading(self):
+        self.paused = True
+
+    def resume_reading(self):
+        self.paused = False
+
+    def get_extra_info(self, k):
+        return ("127.0.0.1", 1)
+
+
+def _proto():
+    from cassmantle_amd.api.wsproto import RFC6455Protocol
+
+    class Cfg:
+        loaded = True
+        loaded_app = staticmethod(lambda *a: None)
+        root_path = ""
+
+    class State:
+        connections = set()
+
+    loop = asyncio.new_event_loop()
+    pr = RFC6455Protocol(Cfg(), State(), {}, _loop=loop)
+    pr.connection_made(_FakeTransport())
+    pr._start = lambda head: setattr(pr, "handshake_done", True)   # no ASGI app needed here
+    return pr, loop
+
+
+def test_protocol_bounds_handshake_queue_and_unmasked():
+    from cassmantle_amd.api import wsproto
+    pr, loop = _proto()
+    pr.data_received(b"GET /clock HTTP/1.1\r\n" + b"X: " + b"y" * (wsproto.MAX_HANDSHAKE + 10))
+    assert pr.transport.closed and b" 431 " in pr.transport.written
+    loop.close()
+    # an application that never reads: reading is paused, then the connection is failed 1008
+    pr, loop = _proto()
+    pr.data_received(b"GET / HTTP/1.1\r\n\r\n")
+    for i in range(wsproto.MAX_QUEUED + 5):
+        if pr.closed:
+            break
+        pr.data_received(_mask(0x1, b"m%d" % i))
+    assert pr.transport.paused or pr.closed
+    assert pr.closed and struct.pack("!H", 1008) in pr.transport.written
+    loop.close()
+    # unmasked frame -> close 1002
+    pr, loop = _proto()
+    pr.data_received(b"GET / HTTP/1.1\r\n\r\n")
+    pr.data_received(_unmasked(0x1, b"hi"))
+    assert pr.closed and struct.pack("!H", 1002) in pr.transport.written
+    loop.close()
