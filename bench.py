@@ -45,6 +45,57 @@ def parse():
     return p.parse_args()
 
 
+def scorer_bench(device) -> dict:
+    """BASELINE config 1 / 5 scorer latency: every timed micro-batch holds DISTINCT guesses drawn
+    from the 49k-word list (no dedup shortcut), against the round's 2 secret words; p50/p99 at
+    batch 1 / 64 / 256 on the GPU (graph-replayed MiniLM), plus the two CPU baselines: the same
+    MiniLM on the CPU for one pair, and the reference-equivalent numpy cosine of 300-d word
+    vectors one pair at a time (``src/backend.py:303-317``)."""
+    import random
+    import numpy as np
+    from cassmantle_amd.scoring.wordvec import load_vocab
+    from cassmantle_amd.game.scoring import score_pairs
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+    words = [w for w in load_vocab() if w.isalpha()]
+    rng = random.Random(0)
+    secrets = ["lantern", "tower"]
+    be = EncoderBackend(device=str(device), stream_priority=-1)
+
+    def run(batch, iters):
+        lat = []
+        for it in range(iters + 3):
+            guesses = rng.sample(words, batch)
+            pairs = [(g, secrets[i % 2]) for i, g in enumerate(guesses)]
+            t1 = time.perf_counter()
+            score_pairs(be, pairs, 0.01)
+            if it >= 3:
+                lat.append((time.perf_counter() - t1) * 1e3)
+        return float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+    out = {}
+    for b in (1, 64, 256):
+        p50, p99 = run(b, 50)
+        out[f"b{b}"] = {"p50_ms": round(p50, 3), "p99_ms": round(p99, 3)}
+    # CPU baselines (config 1)
+    cpu = EncoderBackend(device="cpu")
+    lat = []
+    for _ in range(20):
+        g = rng.choice(words)
+        t1 = time.perf_counter()
+        score_pairs(cpu, [(g, "lantern")], 0.01)
+        lat.append((time.perf_counter() - t1) * 1e3)
+    vec = {w: np.random.default_rng(hash(w) & 0xffff).standard_normal(300).astype(np.float32) for w in words[:2000]}
+    keys = list(vec)
+    lat_np = []
+    for i in range(2000):
+        a, b = vec[keys[i % 2000]], vec[keys[(i * 7 + 1) % 2000]]
+        t1 = time.perf_counter()
+        float(np.dot(a, b) / (np.linalg.norm(a) * np.linalg.norm(b)))
+        lat_np.append((time.perf_counter() - t1) * 1e3)
+    return {"p50_score_ms": out["b64"]["p50_ms"], "p99_score_ms": out["b64"]["p99_ms"], "score_batch": 64,
+            "score_latency": out, "cpu_minilm_1pair_p50_ms": round(float(np.percentile(lat, 50)), 3),
+            "cpu_numpy_cosine_1pair_p50_ms": round(float(np.percentile(lat_np, 50)), 5)}
+
+
 def main() -> int:
     args = parse()
     if args.baseline:
@@ -85,6 +136,8 @@ def main() -> int:
     H = spec.resolution
     gather_buf = None
 
+    gather_ms = []
+
     def one_step(step: int):
         nonlocal gather_buf
         prompts = room_prompts(step)
@@ -93,7 +146,11 @@ def main() -> int:
         if world > 1:
             if gather_buf is None:
                 gather_buf = [torch.empty_like(img) for _ in range(world)]
-            dist.all_gather(gather_buf, img.contiguous())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dist.all_gather(gather_buf, img.contiguous())      # C2: images to the front-end rank
+            e1.record()
+            gather_ms.append((e0, e1))
         return img
 
     for w in range(args.warmup):
@@ -113,29 +170,26 @@ def main() -> int:
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
+    mine = elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    per_rank = None
+    if world > 1:
+        # per-rank step time and all-gather (RCCL over xGMI) time, gathered to rank 0
+        ag = [a.elapsed_time(b) for a, b in gather_ms[args.warmup:]] or [0.0]
+        mine_t = torch.tensor([mine / args.steps * 1e3, float(np.mean(ag))], dtype=torch.float64, device=device)
+        allv = [torch.zeros_like(mine_t) for _ in range(world)]
+        dist.all_gather(allv, mine_t)
+        per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "all_gather_ms": round(float(v[1]), 3)}
+                    for i, v in enumerate(allv)]
     # finiteness of the final LATENTS (the uint8 image is finite by construction)
     finite = bool(sd.last_finite.item()) if sd.last_finite is not None else None
 
     score = {}
     if rank == 0 and not args.no_score:
-        from cassmantle_amd.scoring.encoder import EncoderBackend
-        from cassmantle_amd.game.scoring import score_pairs
-        be = EncoderBackend(device=str(device))
-        words = ["lantern", "river", "ancient", "glowing", "shadow", "ember", "crimson", "tower"]
-        pairs = [(words[i % 8], words[(i * 3 + 1) % 8]) for i in range(64)]
-        for _ in range(5):
-            score_pairs(be, pairs, 0.01)
-        lat = []
-        for _ in range(50):
-            t1 = time.perf_counter()
-            score_pairs(be, pairs, 0.01)
-            lat.append((time.perf_counter() - t1) * 1e3)
-        score = {"p50_score_ms": float(np.percentile(lat, 50)), "p99_score_ms": float(np.percentile(lat, 99)),
-                 "score_batch": len(pairs)}
+        score = scorer_bench(device)    # noqa: F841 - reported below
 
     from cassmantle_amd.utils.tracing import TRACER
     TRACER.flush()
@@ -170,6 +224,9 @@ def main() -> int:
             "stage_mean_ms": stage_ms,      # device time per generation (incl. warmup)
             **score,
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
+            out["comm"] = {"backend": dist.get_backend(), "world_size": world}
         print(json.dumps(out), flush=True)
     cdist.shutdown()
     return 0

@@ -70,6 +70,11 @@ class GameConfig:
     metrics_enabled: bool = False
     num_rooms: int = 1
     snapshot_path: Optional[str] = None   # JSON snapshot at round boundaries
+    # --- multi-GPU failure handling (parallel/rooms.py; reference analog: 120 s lock TTL) ---
+    rank_heartbeat_s: float = 1.0         # period of every rank's heartbeat in the PG store
+    rank_stale_s: float = 30.0            # a heartbeat older than this marks the rank dead
+    round_timeout_s: float = 600.0        # a generation round running longer degrades to local
+    exit_on_rank_failure: bool = False    # after degrading: snapshot + exit 3 for a supervisor
 
 
 @dataclass

@@ -16,10 +16,22 @@ Every message is latency-bound (≤ a few MB), so the protocol uses a fixed, tin
 collectives per round and never sits inside the denoise loop.  With ``backend="nccl"`` these
 are RCCL collectives over xGMI; CPU tests run the identical code on gloo.
 
-Failure handling (SURVEY §5.3): every rank publishes a heartbeat in the process-group store;
-rank 0's :class:`HeartbeatMonitor` reports ranks whose heartbeat is stale and the sharding
-reassigns their rooms to live ranks; a generation round that raises is reported as failed
-so the affected rooms keep their current content (the reference's "round repeats" fallback).
+Failure handling (the reference's analog is the 120 s Redis lock TTL that lets
+another worker take over, ``src/backend.py:47,83-87``):
+
+* every rank publishes a heartbeat in the process-group's TCP store from a side thread (store
+  traffic, never a collective);
+* rank 0's coordinator runs a watchdog: a stale heartbeat, a generation round that outlives
+  ``round_timeout_s`` or a collective that raises puts the coordinator in DEGRADED mode.  A
+  collective with a dead peer cannot be cancelled in-process (RCCL would block until the group
+  timeout), so degraded mode never touches the process group again: pending requests fail at
+  once (the affected rooms keep their current content — the reference's "round repeats"
+  fallback, ``src/backend.py:211-215``) and every later request runs on rank 0's own GPU
+  pipeline (all rooms reassigned to the surviving front-end rank).  The HTTP service never stops;
+  ``on_degraded`` lets the server save a snapshot and, if configured, exit non-zero so a
+  supervisor relaunches a fresh ``torchrun`` group (no process that touched the GPU re-execs);
+* a rank whose generator raises still joins every collective; its rooms' requests fail and
+  those rooms repeat their content.
 """
 from __future__ import annotations
 
@@ -156,23 +168,98 @@ class RankWorker:
 class GenerationCoordinator:
     """Rank 0: turns per-room ``generate`` calls (from the game rooms' worker threads) into
     batched generation rounds, executed on ONE dedicated thread (all collectives are issued
-    from that thread, in order)."""
+    from that thread, in order).  See the module docstring for the degraded mode."""
 
-    def __init__(self, worker: RankWorker, window_s: float = 0.5) -> None:
+    def __init__(self, worker: RankWorker, window_s: float = 0.5, monitor: Optional["HeartbeatMonitor"] = None,
+                 round_timeout_s: float = 600.0, watch_period_s: float = 1.0,
+                 local: Optional[ImageGenerator] = None, on_degraded=None) -> None:
         self.worker = worker
         self.window = window_s
+        self.monitor = monitor
+        self.round_timeout = round_timeout_s
+        self.local = local if local is not None else worker.gen
+        self.on_degraded = on_degraded
+        self.degraded: Optional[str] = None          # reason, once degraded
+        self.round_started: Optional[float] = None
+        self._local_lock = threading.Lock()
+        self._inflight: List[cf.Future] = []
+        self._mu = threading.Lock()
         self._q: "queue.Queue" = queue.Queue()
         self._thread = threading.Thread(target=self._loop, name="gen-coordinator", daemon=True)
         self._stopped = False
         self._thread.start()
+        self._watch_stop = threading.Event()
+        self._watch = None
+        if monitor is not None or round_timeout_s > 0:
+            self._watch = threading.Thread(target=self._watchdog, args=(watch_period_s,), name="gen-watchdog",
+                                           daemon=True)
+            self._watch.start()
+
+    # ------------------------------------------------------------------ failure handling
+    def degrade(self, reason: str) -> None:
+        """Stop using the process group; fail pending work; serve from rank 0's pipeline."""
+        with self._mu:
+            if self.degraded is not None:
+                return
+            self.degraded = reason
+            pending = list(self._inflight)
+            self._inflight.clear()
+        log.error("[ERROR] generation degraded to rank-0-local: %s", reason)
+        try:
+            self.worker.sharding.mark_dead([r for r in range(1, self.worker.ctx.world_size)])
+        except Exception:  # noqa: BLE001
+            pass
+        for fut in pending:
+            if not fut.done():
+                fut.set_exception(ImageGenerationError(f"generation round aborted: {reason}"))
+        while True:                                  # queued, never-started requests too
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if item is not None and not item[3].done():
+                item[3].set_exception(ImageGenerationError(f"generation round aborted: {reason}"))
+        if self.on_degraded is not None:
+            try:
+                self.on_degraded(reason)
+            except Exception:  # noqa: BLE001
+                log.exception("on_degraded callback failed")
+
+    def _watchdog(self, period: float) -> None:
+        while not self._watch_stop.wait(period):
+            if self.degraded is not None:
+                return
+            if self.monitor is not None:
+                try:
+                    dead = [r for r in self.monitor.dead_ranks() if r != self.worker.ctx.rank]
+                except Exception as e:  # noqa: BLE001 - the store itself is gone
+                    dead, err = [-1], e
+                if dead:
+                    self.degrade(f"rank(s) {dead} stopped heart-beating")
+                    return
+            t0 = self.round_started
+            if t0 is not None and self.round_timeout > 0 and time.monotonic() - t0 > self.round_timeout:
+                self.degrade(f"generation round exceeded {self.round_timeout:.0f} s")
+                return
+
+    def generate_local(self, prompts: Sequence[str], seeds: Sequence[int]) -> List[np.ndarray]:
+        with self._local_lock:                       # rank 0's pipeline, one generation at a time
+            return self.local.generate(list(prompts), self.worker.negative, list(seeds))
 
     def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
         fut: cf.Future = cf.Future()
+        if self.degraded is not None:
+            fut.set_exception(ImageGenerationError(f"process group degraded: {self.degraded}"))
+            return fut
+        with self._mu:
+            self._inflight.append(fut)
         self._q.put((room, list(prompts), list(seeds), fut))
         return fut
 
     def _loop(self) -> None:
         while True:
+            if self.degraded is not None:
+                return
             item = self._q.get()
             if item is None:
                 break
@@ -196,25 +283,40 @@ class GenerationCoordinator:
                 start = len(jobs)
                 jobs.extend(GenJob(room, p, s) for p, s in zip(prompts, seeds))
                 spans.append((start, len(jobs), room, fut))
+            self.round_started = time.monotonic()
             try:
                 res = self.worker.run_round(jobs)
                 for s, e, room, fut in spans:
                     imgs = [res.get((room, i)) for i in range(s, e)]
+                    if fut.done():
+                        continue
                     if any(im is None for im in imgs):
                         fut.set_exception(ImageGenerationError(f"room {room}: generation failed"))
                     else:
                         fut.set_result(imgs)
-            except Exception as e:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001 - a collective failed: the group is unusable
                 for *_, fut in spans:
                     if not fut.done():
-                        fut.set_exception(e)
-        self.worker.run_round(STOP)  # type: ignore[arg-type]
+                        fut.set_exception(ImageGenerationError(f"generation round failed: {e}"))
+                self.round_started = None
+                self.degrade(f"collective failed: {type(e).__name__}: {e}")
+                return
+            finally:
+                self.round_started = None
+                with self._mu:
+                    for *_, fut in spans:
+                        if fut in self._inflight:
+                            self._inflight.remove(fut)
+        if self.degraded is None:
+            self.worker.run_round(STOP)  # type: ignore[arg-type]
 
     def close(self) -> None:
         if not self._stopped:
             self._stopped = True
-            self._q.put(None)
-            self._thread.join(timeout=60)
+            self._watch_stop.set()
+            if self.degraded is None:
+                self._q.put(None)
+                self._thread.join(timeout=60)
 
 
 class RankImageGenerator(ImageGenerator):
@@ -227,6 +329,8 @@ class RankImageGenerator(ImageGenerator):
         self.timeout = timeout_s
 
     def generate(self, prompts, negative_prompt, seeds):
+        if self.coord.degraded is not None:          # rooms reassigned to rank 0's own GPU
+            return self.coord.generate_local(prompts, seeds)
         return self.coord.submit(self.room, prompts, seeds).result(timeout=self.timeout)
 
 
@@ -258,6 +362,7 @@ class HeartbeatMonitor:
         self._stop.set()
 
     def dead_ranks(self, now: Optional[float] = None) -> List[int]:
+        """Ranks whose heartbeat is missing or older than ``stale_s`` (wall clock)."""
         now = now or time.time()
         dead = []
         for r in range(self.world):

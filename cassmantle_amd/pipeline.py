@@ -220,17 +220,28 @@ class StableDiffusion:
     @torch.no_grad()
     def generate_tensor(self, prompts: Sequence[str], negative: str, seeds: Sequence[int],
                         steps: Optional[int] = None, guidance: Optional[float] = None,
-                        scheduler: Optional[str] = None) -> torch.Tensor:
-        """-> uint8 [B, H, W, 3] on device (ordered before the caller's current stream)."""
+                        scheduler: Optional[str] = None, sync_caller: bool = True) -> torch.Tensor:
+        """-> uint8 [B, H, W, 3] on device.  With ``sync_caller`` the caller's current stream is
+        made to wait for the generation (the tensor is then safe to use on it); without it the
+        result is ordered only on ``self.stream`` and the caller synchronises that stream.
+
+        Stall root cause (round 1, tools/repro_stall.py, profiles/r2_stall_repro_*.log): a
+        thread with no stream of its own has the process-wide LEGACY default stream as its
+        current stream.  ``caller.wait_stream(self.stream)`` there inserts a wait for the WHOLE
+        denoise loop into that shared stream, so every kernel another thread (the scorer)
+        submits to the legacy stream afterwards queues behind the generation: 28 score batches/s
+        vs 832/s on its own stream, with generation throughput unchanged.  Serving therefore
+        never passes the legacy stream here (``generate`` copies on ``self.stream``), and the
+        scorer always owns a non-blocking stream."""
         plan = make_plan(scheduler or self.spec.scheduler, steps or self.spec.steps,
                          self.spec.guidance if guidance is None else guidance)
         with self._lock:
-            return self._generate_locked(prompts, negative, seeds, plan)
+            return self._generate_locked(prompts, negative, seeds, plan, sync_caller)
 
-    def _generate_locked(self, prompts, negative, seeds, plan) -> torch.Tensor:
+    def _generate_locked(self, prompts, negative, seeds, plan, sync_caller=True) -> torch.Tensor:
         caller = torch.cuda.current_stream(self.device) if self.stream is not None else None
         with (torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()):
-            if caller is not None:
+            if caller is not None and sync_caller:
                 self.stream.wait_stream(caller)     # inputs the caller produced
             # per-stage device time (events on the generation stream: no host sync)
             with span("encode", self.stream):
@@ -241,19 +252,30 @@ class StableDiffusion:
             with span("decode", self.stream):
                 self.last_finite = torch.isfinite(x).all()
                 img = self.vae.decode_uint8(x.to(self.dtype))
-        if caller is not None:
+        if caller is not None and sync_caller:
             caller.wait_stream(self.stream)
             img.record_stream(caller)
         return img
 
     def generate(self, prompts: Sequence[str], negative: str, seeds: Sequence[int], **kw) -> List[np.ndarray]:
         with self._lock:
-            img = self.generate_tensor(prompts, negative, seeds, **kw)
+            img = self.generate_tensor(prompts, negative, seeds, sync_caller=False, **kw)
             finite = self.last_finite
-            arr = img.cpu().numpy()
-            if finite is not None and not bool(finite.item()):
+            if self.stream is not None:
+                # D2H on the generation stream itself and a wait on THAT stream only: nothing is
+                # enqueued on the caller thread's (possibly legacy default) stream
+                with torch.cuda.stream(self.stream):
+                    host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
+                    host.copy_(img, non_blocking=True)
+                    ok = torch.empty((), dtype=torch.bool, pin_memory=True)
+                    ok.copy_(finite, non_blocking=True)
+                self.stream.synchronize()
+                arr, fin = host.numpy(), bool(ok)
+            else:
+                arr, fin = img.numpy(), bool(finite)
+            if not fin:
                 raise ImageGenerationError("non-finite latents (NaN/Inf in the denoise loop)")
-        return [arr[i] for i in range(arr.shape[0])]
+        return [arr[i].copy() for i in range(arr.shape[0])]
 
 
 class DiffusionImageGenerator(ImageGenerator):

@@ -47,25 +47,45 @@ def main(argv=None) -> int:
         return 0
 
     from .parallel import dist as cdist
-    from .parallel.rooms import GenerationCoordinator, RankImageGenerator, RankWorker, RoomSharding
+    from .parallel.rooms import GenerationCoordinator, HeartbeatMonitor, RankImageGenerator, RankWorker, RoomSharding
     ctx = cdist.init_from_env()
     room_ids = [""] + [str(i) for i in range(1, max(cfg.game.num_rooms, world))]
     cfg.game.num_rooms = len(room_ids)
     gen = build_image_generator(cfg, device=str(ctx.device))
     worker = RankWorker(ctx, gen, RoomSharding(room_ids, ctx.world_size), cfg.game.negative_prompt)
+    import torch.distributed as tdist
+    store = tdist.distributed_c10d._get_default_store()
+    hb = HeartbeatMonitor(store, ctx.rank, ctx.world_size, period_s=cfg.game.rank_heartbeat_s,
+                          stale_s=cfg.game.rank_stale_s).start()
     if ctx.rank != 0:
         worker.serve_forever()
+        hb.stop()
         cdist.shutdown()
         return 0
-    coord = GenerationCoordinator(worker)
+    holder = {}
+
+    def on_degraded(reason: str) -> None:
+        # rooms keep serving from rank 0's GPU; optionally hand over to a supervisor restart
+        svc_ = holder.get("svc")
+        if svc_ is not None:
+            svc_.save_snapshot()
+        if cfg.game.exit_on_rank_failure:
+            logging.getLogger("cassmantle").error("[ERROR] exiting for a supervisor restart: %s", reason)
+            os._exit(3)   # the collectives are unusable; no barrier / destroy on a dead group
+
+    coord = GenerationCoordinator(worker, monitor=hb, round_timeout_s=cfg.game.round_timeout_s,
+                                  on_degraded=on_degraded)
     svc = build_service(cfg, image_gen_for_room=lambda rid: RankImageGenerator(coord, rid), room_ids=room_ids)
+    holder["svc"] = svc
     app = create_app(svc, cfg)
     try:
         uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
     finally:
         coord.close()
-        cdist.shutdown()
-    return 0
+        hb.stop()
+        if coord.degraded is None:
+            cdist.shutdown()
+    return 0 if coord.degraded is None else 3
 
 
 if __name__ == "__main__":

@@ -99,3 +99,42 @@ def test_unet_is_bit_deterministic_run_to_run():
         a = m(x, t, ctx)
         b = m(x, t, ctx)
     assert torch.equal(a, b)
+
+
+def test_legacy_stream_scorer_not_blocked_by_generation():
+    """the round-1 'stall': a scorer on the thread's LEGACY default stream while another thread
+    generates.  generate() must not enqueue anything on the legacy stream, so scoring keeps its
+    latency while a generation is in flight (it queued behind whole generations before)."""
+    import threading
+    import time
+    import numpy as np
+    from cassmantle_amd.game.scoring import score_pairs
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+    sd = StableDiffusion(SPECS["sd15"], device="cuda", seed=0)
+    sd.generate(["a lantern"] * 2, "blurry", [0, 1], steps=4)          # capture
+    be = EncoderBackend(device="cuda", use_graphs=False)
+    be.stream = None                                                    # legacy default stream
+    pairs = [(w, "tower") for w in ("lantern", "river", "ember", "shadow")]
+    score_pairs(be, pairs, 0.01)
+    stop = threading.Event()
+    gens = [0]
+
+    def loop():
+        while not stop.is_set():
+            sd.generate(["a lantern"] * 2, "blurry", [2, 3], steps=12)
+            gens[0] += 1
+    th = threading.Thread(target=loop, daemon=True)
+    th.start()
+    time.sleep(0.5)
+    lat = []
+    t_end = time.perf_counter() + 6.0
+    while time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        score_pairs(be, pairs, 0.01)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    stop.set()
+    th.join(timeout=60)
+    assert gens[0] >= 1
+    # one 12-step generation of 2 images takes ~100 ms: queueing behind it would put p50 there
+    assert len(lat) > 200 and float(np.percentile(lat, 50)) < 20.0, (len(lat), np.percentile(lat, 50))

@@ -4,6 +4,7 @@ coordinator that batches rooms' requests, heartbeat-based dead-rank reassignment
 import os
 import socket
 import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -100,3 +101,123 @@ def test_generation_rounds_gloo(world, fail_rank):
     assert rounds >= 1
     # only rank 0 heart-beat in this test -> the others are reported
     assert 0 not in dead
+
+
+# ---------------------------------------------------------------- a worker process dies mid-round
+class _KillableGen(SolidImageGenerator):
+    """Rank 1 exits the whole process (no cleanup, like an OOM kill or a crashed driver) on
+    its first generation after rank 0 drops a trigger file."""
+
+    def __init__(self, rank, trigger, res=16, mode="kill"):
+        super().__init__(res)
+        self.rank, self.trigger, self.mode = rank, trigger, mode
+        self.hb = None
+
+    def generate(self, prompts, negative, seeds):
+        if self.rank == 1 and os.path.exists(self.trigger):
+            if self.mode == "kill":
+                os._exit(17)
+            self.hb.stop()                          # "hang": a wedged rank (no heartbeat, no error):
+            time.sleep(600)                         # its peers' collective would block until timeout
+        out = super().generate(prompts, negative, seeds)
+        for im in out:
+            im[:8, :8, :] = 255 * self.rank          # survives JPEG: the drawing rank's mark
+        return out
+
+
+def _serve_rank(rank, world, port, rooms, result_path, trigger, mode):
+    import asyncio
+    from fastapi.testclient import TestClient
+    from cassmantle_amd.api.app import create_app
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.game.imaging import decode_jpeg
+    from cassmantle_amd.game.service import GameService
+    from cassmantle_amd.scoring.batcher import BatchingScorer
+    from cassmantle_amd.scoring.wordvec import WordVectorBackend
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = DistContext(rank, world, rank, torch.device("cpu"), "gloo")
+    store = dist.distributed_c10d._get_default_store()
+    hb = HeartbeatMonitor(store, rank, world, period_s=0.2, stale_s=3.0).start()
+    gen = _KillableGen(rank, trigger, mode=mode)
+    gen.hb = hb
+    worker = RankWorker(ctx, gen, RoomSharding(rooms, world))
+    if rank != 0:
+        worker.serve_forever()
+        os._exit(0)
+    degraded = []
+    coord = GenerationCoordinator(worker, window_s=0.3, monitor=hb, round_timeout_s=60, watch_period_s=0.2,
+                                  on_degraded=degraded.append)
+    cfg = Config()
+    cfg.game.rate_limit_enabled = False
+    cfg.game.max_retries = 1
+    cfg.game.num_rooms = len(rooms)
+    be = WordVectorBackend(vocab=["lantern", "tower"], vectors=np.eye(2, dtype=np.float32))
+    svc = GameService(cfg, BatchingScorer(be, cfg.game.min_score),
+                      image_gen_for_room=lambda rid: RankImageGenerator(coord, rid, timeout_s=60), room_ids=rooms, seed=0)
+    client = TestClient(create_app(svc, cfg, run_timers=False))
+    res = {}
+
+    def tags():
+        return {r: int(decode_jpeg(svc.room(r).store.hget(svc.room(r).k("image"), "current"))[:8, :8].mean() > 128)
+                for r in rooms}
+
+    def versions():
+        return {r: svc.room(r).store.hget(svc.room(r).k("image"), "version") for r in rooms}
+
+    async def next_round():
+        ok = await asyncio.gather(*(svc.room(r).buffer_contents() for r in rooms))
+        for r in rooms:
+            await svc.room(r).end_round()
+        return list(ok)
+
+    with client:                                           # startup: round 1, both ranks alive
+        res["start_rank1_rooms"] = tags()
+        v1 = versions()
+        open(trigger, "w").close()                         # rank 1 dies in the next round
+        res["round2_ok"] = client.portal.call(next_round)
+        v2 = versions()
+        res["repeated"] = [r for r in rooms if v2[r] == v1[r]]
+        res["degraded"] = list(degraded)
+        # the HTTP service keeps answering every room
+        res["http"] = [client.get(f"/fetch/contents?room={r}").status_code for r in rooms]
+        res["round3_ok"] = client.portal.call(next_round)   # all rooms now on rank 0's pipeline
+        v3 = versions()
+        res["round3_new"] = [r for r in rooms if v3[r] != v2[r]]
+        res["round3_rank1_tags"] = tags()
+    with open(result_path, "w") as f:
+        f.write(repr(res))
+    hb.stop()
+    os._exit(0)                                            # never barrier on a dead group
+
+
+@pytest.mark.parametrize("mode", ["kill", "hang"])
+def test_worker_killed_mid_round_rank0_keeps_serving(mode):
+    """a rank process dies ("kill": the failed collective raises) or wedges without an error
+    ("hang": only its stale heartbeat tells, as with RCCL blocking on a dead peer) during a
+    generation round: rank 0 degrades, the round's rooms repeat their content, the HTTP service
+    keeps answering, and later rounds run every room on rank 0's own pipeline"""
+    import multiprocessing as pymp
+    rooms = ["", "1", "2", "3"]
+    ctx = pymp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        path, trig = os.path.join(d, "res.txt"), os.path.join(d, "die")
+        port = free_port()
+        ps = [ctx.Process(target=_serve_rank, args=(r, 2, port, rooms, path, trig, mode)) for r in range(2)]
+        for p in ps:
+            p.start()
+        ps[0].join(timeout=180)
+        ps[1].join(timeout=5 if mode == "hang" else 60)
+        codes = [p.exitcode for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+        assert codes[0] == 0 and codes[1] == (17 if mode == "kill" else None), codes
+        res = eval(open(path).read())
+    assert res["start_rank1_rooms"] == {"": 0, "1": 1, "2": 0, "3": 1}    # rooms 1, 3 drawn by rank 1
+    assert res["degraded"] and not all(res["round2_ok"])
+    assert set(res["repeated"]) >= {"1", "3"}               # rank 1's rooms repeat their round
+    assert res["http"] == [200] * 4
+    assert all(res["round3_ok"]) and set(res["round3_new"]) == set(rooms)
+    assert res["round3_rank1_tags"] == {r: 0 for r in rooms}    # everything drawn by rank 0

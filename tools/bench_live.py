@@ -1,15 +1,16 @@
 """BASELINE config 5: a live round — image generation and streaming guess scoring overlapped.
 
-Each rank (one per GPU, ``torchrun`` for N > 1) owns its rooms' content generation AND the
-guess scoring of its rooms' players:
+The SERVING topology (``serve.py``): every rank (one per GPU, ``torchrun`` for N > 1) generates
+its rooms' content; ALL guess scoring runs on rank 0, next to the front-end that owns every
+session (a guess costs microseconds of GPU time, so a cross-rank hop would only add latency):
 
-* a generation thread replays the hipGraph-captured SD-1.5 denoise loop back to back
-  (batch 4 images per room, 512², 50 PNDM steps) on the default stream;
-* an asyncio loop runs ``players / world`` simulated players per rank; each submits its two
-  mask guesses, waits for the scores, "thinks" for a random 0.5–1.5 × ``--think-ms`` and
-  repeats.  Requests go through the micro-batching scorer (``scoring.batcher``), whose MiniLM
-  embed + cosine runs on a HIGH-PRIORITY stream (``EncoderBackend(stream_priority=-1)``) so
-  scoring kernels are dispatched ahead of queued denoise kernels.
+* on every rank a generation thread replays the hipGraph-captured SD-1.5 denoise loop back to
+  back (batch 4 images per room, 512², 50 PNDM steps) on the pipeline's own stream;
+* on rank 0 an asyncio loop runs ``--players`` simulated players; each submits its two mask
+  guesses, waits for the scores, "thinks" for a random 0.5–1.5 × ``--think-ms`` and repeats.
+  Requests go through the micro-batching scorer (``scoring.batcher``), whose graph-replayed
+  MiniLM embed + cosine runs on a HIGH-PRIORITY stream (``EncoderBackend(stream_priority=-1)``)
+  so scoring kernels are dispatched ahead of queued denoise kernels.
 
 Phases: ``--idle-s`` seconds of scoring alone (latency floor), then ``--seconds`` with both.
 Rank 0 prints one JSON line: whole-job images/s during the overlapped phase, p50/p99 guess
@@ -43,9 +44,9 @@ def parse():
     ap.add_argument("--model", default="sd15")
     ap.add_argument("--priority", type=int, default=-1, help="scorer stream priority (lower = higher)")
     ap.add_argument("--no-priority", action="store_true",
-                    help="A/B: score on a normal-priority side stream.  (Scoring on the legacy default "
-                         "stream while the generation thread replays graphs stalled the process on "
-                         "MI355X in two runs; the serving stack never does that.)")
+                    help="A/B: score on a normal-priority side stream (the scorer always owns a stream: "
+                         "on the legacy default stream it queued behind whole generations, "
+                         "pipeline.StableDiffusion.generate_tensor docstring)")
     ap.add_argument("--window-ms", type=float, default=1.0)
     return ap.parse_args()
 
@@ -81,7 +82,7 @@ def main():
 
     ctx = cdist.init_from_env()
     rank, world, dev = ctx.rank, ctx.world_size, ctx.device
-    n_players = a.players // world + (1 if rank < a.players % world else 0)
+    n_players = a.players if rank == 0 else 0          # rank-0-central scoring, as serve.py
     sd = StableDiffusion(SPECS[a.model], device=dev, seed=0)
     backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
     scorer = BatchingScorer(backend, 0.01, window_ms=a.window_ms)
@@ -96,13 +97,14 @@ def main():
 
     # warm everything (graph capture, allocator, scorer shapes)
     sd.generate_tensor(prompts(0), neg, list(range(a.batch))).cpu()
-    asyncio.run(run_players(scorer, min(n_players, 4), 1.0, a.think_ms, rank + 99))
+    if n_players:
+        asyncio.run(run_players(scorer, min(n_players, 4), 1.0, a.think_ms, rank + 99))
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
 
-    idle = asyncio.run(run_players(scorer, n_players, a.idle_s, a.think_ms, rank))
+    idle = asyncio.run(run_players(scorer, n_players, a.idle_s, a.think_ms, rank)) if n_players else []
 
     done = {"images": 0}
     stop = threading.Event()
@@ -110,8 +112,8 @@ def main():
     def gen_loop():
         step = 1
         while not stop.is_set():
-            img = sd.generate_tensor(prompts(step), neg, [rank * 10000 + step * 10 + j for j in range(a.batch)])
-            img.cpu()                       # completes this batch (blocks this thread only)
+            # numpy result copied on the generation stream: never waits on the legacy stream
+            sd.generate(prompts(step), neg, [rank * 10000 + step * 10 + j for j in range(a.batch)])
             done["images"] += a.batch
             step += 1
 
@@ -120,7 +122,11 @@ def main():
     th = threading.Thread(target=gen_loop, daemon=True)
     t0 = time.perf_counter()
     th.start()
-    load = asyncio.run(run_players(scorer, n_players, a.seconds, a.think_ms, rank + 7))
+    if n_players:
+        load = asyncio.run(run_players(scorer, n_players, a.seconds, a.think_ms, rank + 7))
+    else:
+        load = []
+        time.sleep(a.seconds)
     imgs_at_stop = done["images"]
     elapsed = time.perf_counter() - t0
     stop.set()
@@ -135,7 +141,7 @@ def main():
         allv = [torch.zeros_like(stats) for _ in range(world)]
         torch.distributed.all_gather(allv, stats)
         m = torch.stack(allv)
-        agg = [m[:, 0].sum(), m[:, 1].max(), m[:, 2].max(), m[:, 3].max(), m[:, 4].max(), m[:, 5].sum()]
+        agg = [m[:, 0].sum(), m[0, 1], m[0, 2], m[0, 3], m[0, 4], m[:, 5].sum()]   # latencies: rank 0 scores
         stats = torch.stack(agg)
     if rank == 0:
         s = [float(x) for x in stats.tolist()]
