@@ -125,7 +125,22 @@ class Conv2d(nn.Module):
             self._w4_key = key
         return self._w4
 
+    _wpad = None   # weight zero-padded to a channel-padded input (UNet conv_in: 4 -> 8 channels)
+    _wpad_key = None
+
+    def padded_weight(self, cin: int):
+        key = (self.weight.data_ptr(), self.weight._version, cin)
+        if self._wpad is None or self._wpad_key != key:
+            self._wpad = torch.nn.functional.pad(self.weight, (0, cin - self.cin)).contiguous()
+            self._wpad_key = key
+        return self._wpad
+
     def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None):
+        if x.shape[-1] > self.cin:
+            # input carries zero padding channels (graph-static UNet input): padded weights,
+            # cached, instead of a pad copy of input and weight on every call
+            return ops.conv2d(x, self.padded_weight(x.shape[-1]), self.bias, self.stride, self.padding,
+                              residual=residual, upsample=upsample, chan_bias=chan_bias, stats=stats)
         if upsample and self.k == 3 and self.stride == 1 and _UP2 and x.device.type == "cuda" \
                 and ops.get_mode() == "hip" and self.cin % 64 == 0:
             # nearest-2x upsample + 3x3 conv as four parity-class 2x2 convs (4/9 of the MACs)

@@ -162,9 +162,10 @@ def latent_step_reference(eps, x, hist, xs, coef, step, unet_in, cfg: bool) -> N
     if r[12] > 0:
         xs.copy_(x_old)
     nxt = (r[7] * x).to(unet_in.dtype)
+    C = x.shape[-1]                  # unet_in may carry zero padding channels beyond C
     if cfg:
         B = x.shape[0]
-        unet_in[:B].copy_(nxt)
-        unet_in[B:].copy_(nxt)
+        unet_in[:B, ..., :C].copy_(nxt)
+        unet_in[B:, ..., :C].copy_(nxt)
     else:
-        unet_in.copy_(nxt)
+        unet_in[..., :C].copy_(nxt)

@@ -585,15 +585,23 @@ def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, 
 
 
 def latent_step(eps: torch.Tensor, x: torch.Tensor, hist: torch.Tensor, xs: torch.Tensor,
-                coef: torch.Tensor, step: torch.Tensor, unet_in: torch.Tensor, cfg: bool) -> None:
+                coef: torch.Tensor, step: torch.Tensor, unet_in: torch.Tensor, cfg: bool,
+                rows=None) -> None:
     """Fused CFG-combine + scheduler update + next-step UNet-input write (see
-    ``models/schedulers.py`` for the coefficient-table contract).  In place on x/hist/xs/unet_in.
-    ``step`` is a device int32 scalar so the whole step is graph-capturable."""
+    ``models/schedulers.py`` for the coefficient-table contract).  In place on x/hist/xs/unet_in;
+    ``unet_in`` may be channel-padded (its extra channels stay zero).  ``rows``: up to two
+    ``(table [E, ...], buffer)`` pairs — row ``min(step + 1, E - 1)`` of each table is copied into
+    its buffer by the same launch (the next step's time conditioning).  ``step`` is a device
+    int32 scalar so the whole step is graph-capturable."""
+    rows = list(rows or [])
     if not _use_hip(x):
         from ..models.schedulers import latent_step_reference
         latent_step_reference(eps, x, hist, xs, coef, step, unet_in, cfg)
+        for tab, buf in rows:
+            buf.copy_(tab[min(int(step.item()) + 1, tab.shape[0] - 1)].view_as(buf))
         return
-    ext().latent_step(eps, x, hist, xs, coef, step, unet_in, int(cfg))
+    (t0, b0), (t1, b1) = (rows + [(None, None), (None, None)])[:2]
+    ext().latent_step(eps, x, hist, xs, coef, step, unet_in, int(cfg), t0, b0, t1, b1)
 
 
 def advance_step(step: torch.Tensor) -> None:

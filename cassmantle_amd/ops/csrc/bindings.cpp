@@ -451,16 +451,33 @@ void timestep_embedding(const at::Tensor& t, at::Tensor& out, int64_t flip, doub
 }
 
 void latent_step(const at::Tensor& eps, at::Tensor& x, at::Tensor& hist, at::Tensor& xs, const at::Tensor& coef,
-                 const at::Tensor& step, at::Tensor& unet_in, int64_t cfg) {
-  CHECK_DEV(x); CHECK_BF16(eps); CHECK_CONTIG(eps); CHECK_BF16(unet_in);
+                 const at::Tensor& step, at::Tensor& unet_in, int64_t cfg, const c10::optional<at::Tensor>& tab0,
+                 const c10::optional<at::Tensor>& buf0, const c10::optional<at::Tensor>& tab1,
+                 const c10::optional<at::Tensor>& buf1) {
+  CHECK_DEV(x); CHECK_BF16(eps); CHECK_CONTIG(eps); CHECK_BF16(unet_in); CHECK_CONTIG(unet_in);
   TORCH_CHECK(x.scalar_type() == at::kFloat && hist.scalar_type() == at::kFloat && xs.scalar_type() == at::kFloat,
               "latent_step: f32 master latents");
   TORCH_CHECK(step.scalar_type() == at::kInt, "latent_step: int32 step counter");
   const long long n = x.numel();
-  TORCH_CHECK(eps.numel() == (cfg ? 2 * n : n) && unet_in.numel() == eps.numel() && hist.numel() == 4 * n,
-              "latent_step: shape mismatch");
+  const int cin = (int)x.size(-1), cstride = (int)unet_in.size(-1);
+  TORCH_CHECK(cstride >= cin && eps.numel() == (cfg ? 2 * n : n) && hist.numel() == 4 * n &&
+              unet_in.numel() == eps.numel() / cin * cstride, "latent_step: shape mismatch");
+  auto tab_ok = [&](const c10::optional<at::Tensor>& t, const c10::optional<at::Tensor>& b) {
+    if (!t.has_value() || !t->defined()) return false;
+    TORCH_CHECK(b.has_value() && b->defined() && t->is_contiguous() && b->is_contiguous() &&
+                t->numel() % t->size(0) == 0 && b->numel() * b->element_size() * t->size(0) == t->numel() * t->element_size() &&
+                (b->numel() * b->element_size()) % 16 == 0, "latent_step: tables [rows, ...] and row buffers, 16-B rows");
+    return true;
+  };
+  const bool h0 = tab_ok(tab0, buf0), h1 = tab_ok(tab1, buf1);
+  const int rows = h0 ? (int)tab0->size(0) : (h1 ? (int)tab1->size(0) : 0);
+  TORCH_CHECK(!(h0 && h1) || tab1->size(0) == rows, "latent_step: tables of equal row count");
   launch_latent_step(bptr(eps), x.data_ptr<float>(), hist.data_ptr<float>(), xs.data_ptr<float>(),
-                     coef.data_ptr<float>(), step.data_ptr<int>(), bptr_mut(unet_in), n, (int)cfg, cur_stream());
+                     coef.data_ptr<float>(), step.data_ptr<int>(), bptr_mut(unet_in), n, (int)cfg, cin, cstride,
+                     h0 ? tab0->data_ptr() : nullptr, h0 ? buf0->data_ptr() : nullptr,
+                     h0 ? buf0->numel() * buf0->element_size() : 0, h1 ? tab1->data_ptr() : nullptr,
+                     h1 ? buf1->data_ptr() : nullptr, h1 ? buf1->numel() * buf1->element_size() : 0, rows,
+                     cur_stream());
 }
 
 void advance_step(at::Tensor& step) { launch_advance_step(step.data_ptr<int>(), cur_stream()); }

@@ -142,8 +142,12 @@ void launch_gaussian_blur(const void* img, int u8, int H, int W, int C, const fl
                           float* tmp, void* out, hipStream_t s);
 void launch_to_uint8(const uint16_t* x, uint8_t* out, long long n, hipStream_t s);
 void launch_timestep_embedding(const float* t, float* out, int B, int dim, int flip, float shift, hipStream_t s);
-void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef,
-                        const int* step, uint16_t* unet_in, long long n, int cfg, hipStream_t s);
+// CFG combine + scheduler update + next UNet input (channel-padded to cstride); the optional
+// tables' rows for step+1 (time conditioning) are copied into buf0/buf1 by extra blocks
+void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef, const int* step,
+                        uint16_t* unet_in, long long n, int cfg, int cin, int cstride, const void* tab0, void* buf0,
+                        long long row_bytes0, const void* tab1, void* buf1, long long row_bytes1, int rows,
+                        hipStream_t s);
 void launch_advance_step(int* step, hipStream_t s);
 void launch_softmax_rows(const float* S, uint16_t* P, int rows, int cols, int Nq, int causal,
                          const int* kv_lens, hipStream_t s);

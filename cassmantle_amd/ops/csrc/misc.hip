@@ -157,10 +157,32 @@ __global__ void timestep_embedding_kernel(const float* __restrict__ t, float* __
 }
 
 // coefficient row layout: see models/schedulers.py
+// Per-step time-conditioning rows: the next step's rows of up to two per-plan tables are copied
+// into the fixed buffers the captured UNet reads (replaces an int->long cast + 2 index_select
+// launches per step); these are extra blocks of the latent-step launch.
+struct StepRows {
+  const uint4* tab[2] = {nullptr, nullptr};
+  uint4* buf[2] = {nullptr, nullptr};
+  int row_units[2] = {0, 0};     // 16-byte units per row
+  int rows = 0;                  // table rows (plan evals)
+};
+
 __global__ void latent_step_kernel(const uint16_t* __restrict__ eps, float* __restrict__ x,
                                    float* __restrict__ hist, float* __restrict__ xs,
                                    const float* __restrict__ coef, const int* __restrict__ step,
-                                   uint16_t* __restrict__ unet_in, long long n, int cfg) {
+                                   uint16_t* __restrict__ unet_in, long long n, int cfg, int cin, int cstride,
+                                   int latent_blocks, StepRows rows) {
+  if ((int)blockIdx.x >= latent_blocks) {                   // next step's conditioning rows
+    const int s = min(step[0] + 1, rows.rows - 1);
+    const long long b = (long long)(blockIdx.x - latent_blocks) * blockDim.x + threadIdx.x;
+    const long long tot0 = rows.row_units[0];
+    if (b < tot0) {
+      rows.buf[0][b] = rows.tab[0][(long long)s * tot0 + b];
+    } else if (b - tot0 < rows.row_units[1]) {
+      rows.buf[1][b - tot0] = rows.tab[1][(long long)s * rows.row_units[1] + (b - tot0)];
+    }
+    return;
+  }
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* r = coef + 16 * step[0];
@@ -182,8 +204,12 @@ __global__ void latent_step_kernel(const uint16_t* __restrict__ eps, float* __re
   if (r[12] > 0.f) xs[i] = xo;
   x[i] = xn;
   uint16_t o = f2bf(r[7] * xn);
-  unet_in[i] = o;
-  if (cfg) unet_in[n + i] = o;
+  // the UNet input may be channel-padded (cstride 8 > cin 4: conv_in's K in whole 16-byte
+  // chunks without a per-step pad copy); padding channels stay zero
+  const long long ui = (i / cin) * cstride + (i % cin);
+  const long long un = (n / cin) * cstride;
+  unet_in[ui] = o;
+  if (cfg) unet_in[un + ui] = o;
 }
 
 __global__ void advance_step_kernel(int* step) { step[0] += 1; }
@@ -352,9 +378,19 @@ void launch_timestep_embedding(const float* t, float* out, int B, int dim, int f
 }
 
 void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef, const int* step,
-                        uint16_t* unet_in, long long n, int cfg, hipStream_t s) {
-  hipLaunchKernelGGL(latent_step_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, eps, x, hist, xs, coef, step, unet_in,
-                     n, cfg);
+                        uint16_t* unet_in, long long n, int cfg, int cin, int cstride, const void* tab0, void* buf0,
+                        long long row_bytes0, const void* tab1, void* buf1, long long row_bytes1, int rows,
+                        hipStream_t s) {
+  StepRows r;
+  r.tab[0] = reinterpret_cast<const uint4*>(tab0); r.buf[0] = reinterpret_cast<uint4*>(buf0);
+  r.tab[1] = reinterpret_cast<const uint4*>(tab1); r.buf[1] = reinterpret_cast<uint4*>(buf1);
+  r.row_units[0] = tab0 ? (int)(row_bytes0 / 16) : 0;
+  r.row_units[1] = tab1 ? (int)(row_bytes1 / 16) : 0;
+  r.rows = rows;
+  const int lb = (int)nblk(n, 256);
+  const int cb = (int)nblk((long long)r.row_units[0] + r.row_units[1], 256);
+  hipLaunchKernelGGL(latent_step_kernel, dim3(lb + cb), dim3(256), 0, s, eps, x, hist, xs, coef, step, unet_in, n,
+                     cfg, cin, cstride, lb, r);
 }
 
 void launch_advance_step(int* step, hipStream_t s) {

@@ -65,7 +65,10 @@ class _StepState:
         self.x = torch.zeros((B, h, w, 4), device=device, dtype=torch.float32)
         self.xs = torch.zeros_like(self.x)
         self.hist = torch.zeros((4, B, h, w, 4), device=device, dtype=torch.float32)
-        self.unet_in = torch.zeros((nb, h, w, 4), device=device, dtype=dtype)
+        # on the GPU the UNet input carries 4 zero channels: conv_in then reads whole 16-byte
+        # k-chunks with no per-step pad copy (the latent-step kernel writes channels 0..3)
+        self.unet_in = torch.zeros((nb, h, w, 8 if torch.device(device).type == "cuda" else 4), device=device,
+                                   dtype=dtype)
         self.ctx = torch.zeros_like(ctx)
         self.coef = torch.from_numpy(plan.table).to(device)
         self.tsteps = torch.from_numpy(plan.table[:, 14].copy()).to(device)
@@ -78,10 +81,14 @@ class _StepState:
         # per-plan time conditioning (UNet.time_table), refilled in place every generation
         self.temb_tab: Optional[torch.Tensor] = None
         self.tb_tab: Optional[torch.Tensor] = None
+        # the current step's rows, refilled by the latent-step launch for the next step
+        self.temb_cur: Optional[torch.Tensor] = None
+        self.tb_cur: Optional[torch.Tensor] = None
 
     def load_time(self, temb: torch.Tensor, tb: torch.Tensor) -> None:
         if self.temb_tab is None:
             self.temb_tab, self.tb_tab = temb.clone(), tb.clone()
+            self.temb_cur, self.tb_cur = temb[0].clone(), tb[0].clone()
         else:
             self.temb_tab.copy_(temb)
             self.tb_tab.copy_(tb)
@@ -92,11 +99,15 @@ class _StepState:
         self.hist.zero_()
         self.ctx.copy_(ctx)
         nxt = (x0 * self.plan.c_in0).to(self.unet_in.dtype)
+        C = x0.shape[-1]
         if self.cfg:
-            self.unet_in[: self.B].copy_(nxt)
-            self.unet_in[self.B:].copy_(nxt)
+            self.unet_in[: self.B, ..., :C].copy_(nxt)
+            self.unet_in[self.B:, ..., :C].copy_(nxt)
         else:
-            self.unet_in.copy_(nxt)
+            self.unet_in[..., :C].copy_(nxt)
+        if self.temb_tab is not None:
+            self.temb_cur.copy_(self.temb_tab[0])
+            self.tb_cur.copy_(self.tb_tab[0])
         if added is not None:
             for k, v in added.items():
                 self.added[k].copy_(v)
@@ -154,11 +165,11 @@ class StableDiffusion:
 
     # ------------------------------------------------------------------ denoise
     def _unet_step(self, st: _StepState) -> None:
-        idx = st.step.long()
-        # this step's rows of the per-plan time table (device index: graph-capturable)
-        cond = (st.temb_tab.index_select(0, idx)[0], st.tb_tab.index_select(0, idx)[0])
-        eps = self.unet(st.unet_in, None, st.ctx, st.added, fp8=self.fp8, time_cond=cond)
-        ops.latent_step(eps, st.x, st.hist, st.xs, st.coef, st.step, st.unet_in, st.cfg)
+        # this step's rows of the per-plan time tables (st.*_cur: filled for step 0 by load(),
+        # then by the previous step's latent-step launch from the device step counter)
+        eps = self.unet(st.unet_in, None, st.ctx, st.added, fp8=self.fp8, time_cond=(st.temb_cur, st.tb_cur))
+        ops.latent_step(eps, st.x, st.hist, st.xs, st.coef, st.step, st.unet_in, st.cfg,
+                        rows=[(st.temb_tab, st.temb_cur), (st.tb_tab, st.tb_cur)])
         ops.advance_step(st.step)
 
     def _state(self, B: int, ctx: torch.Tensor, plan: SchedulePlan, added) -> _StepState:

@@ -486,3 +486,33 @@ def test_gpu_blur_fn_serves_blur_cache():
     assert cache.prewarm("v1", jpeg, 15.0) == 16
     assert cache.misses == 16 and decode_jpeg(cache.get("v1", jpeg, 3.2)).shape == (1024, 1024, 3)
     assert cache.hits >= 1
+
+
+def test_latent_step_padded_input_and_row_select():
+    """channel-padded UNet input (cstride 8: channels 4..7 stay zero) and the next step's
+    time-conditioning rows copied by the same launch (clamped at the last row)"""
+    from cassmantle_amd.models.schedulers import make_plan
+    plan = make_plan("pndm", 6, 7.5)
+    B = 2
+    x = torch.randn(B, 8, 8, 4, generator=torch.Generator().manual_seed(41)).to(DEV)
+    x4 = x.clone()
+    hist, xs = torch.zeros(4, B, 8, 8, 4, device=DEV), torch.zeros(B, 8, 8, 4, device=DEV)
+    hist4, xs4 = hist.clone(), xs.clone()
+    u8 = torch.zeros(2 * B, 8, 8, 8, device=DEV, dtype=torch.bfloat16)
+    u4 = torch.zeros(2 * B, 8, 8, 4, device=DEV, dtype=torch.bfloat16)
+    coef = torch.from_numpy(plan.table).to(DEV)
+    E = plan.evals
+    tab0 = torch.randn(E, 2 * B, 320, generator=torch.Generator().manual_seed(42)).to(torch.bfloat16).to(DEV)
+    tab1 = torch.randn(E, 2 * B, 1000, generator=torch.Generator().manual_seed(43)).to(torch.bfloat16).to(DEV)
+    b0, b1 = tab0[0].clone(), tab1[0].clone()
+    step, step4 = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    for i in range(E):
+        eps = torch.randn(2 * B, 8, 8, 4, generator=torch.Generator().manual_seed(200 + i)).to(torch.bfloat16).to(DEV)
+        ops.latent_step(eps, x, hist, xs, coef, step, u8, True, rows=[(tab0, b0), (tab1, b1)])
+        ops.latent_step(eps, x4, hist4, xs4, coef, step4, u4, True)
+        ops.advance_step(step)
+        ops.advance_step(step4)
+        nxt = min(i + 1, E - 1)
+        assert torch.equal(b0, tab0[nxt]) and torch.equal(b1, tab1[nxt])
+        assert torch.equal(u8[..., :4], u4) and not u8[..., 4:].any()
+    assert torch.equal(x, x4)

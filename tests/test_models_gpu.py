@@ -79,11 +79,83 @@ def test_pipeline_graph_replay_matches_eager():
     assert torch.allclose(b, c)
 
 
-def test_sd15_end_to_end_one_image():
+def _fp32_cpu_copy(m):
+    import copy
+    c = copy.deepcopy(m).float().cpu()
+    return c
+
+
+def test_sd15_unet_full_size_vs_fp32_reference():
+    """ONE full SD-1.5 UNet evaluation (batch 1, 64^2 latent, 77-token context) on the HIP
+    kernels vs the same weights through the fp32 PyTorch reference ops on the CPU"""
+    from cassmantle_amd.models.unet import SD15_UNET, UNet
+    m = UNet(SD15_UNET, seed=0).cuda()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1, 64, 64, 4, generator=g).to(torch.bfloat16)
+    t = torch.tensor([601.0])
+    ctx = (torch.randn(1, 77, 768, generator=g) * 0.5).to(torch.bfloat16)
+    with torch.no_grad():
+        out = m(x.cuda(), t.cuda(), ctx.cuda()).float().cpu()
+        ref = _fp32_cpu_copy(m)(x.float(), t, ctx.float())
+    assert torch.isfinite(out).all()
+    c = cos(out, ref)
+    assert c >= 0.999, c
+
+
+def test_sd_vae_decoder_full_size_vs_fp32_reference():
+    """the full SD VAE decoder (64^2 latent -> 512^2 image: 512-channel convs, the d=512
+    mid-block attention, the parity upsampling convs) vs the fp32 reference"""
+    from cassmantle_amd.models.vae import SD_VAE, VAEDecoder
+    vae = VAEDecoder(SD_VAE, seed=1).cuda()
+    z = torch.randn(1, 64, 64, 4, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
+    with torch.no_grad():
+        out = vae(z.cuda()).float().cpu()
+        ref = _fp32_cpu_copy(vae)(z.float())
+    assert out.shape == ref.shape == (1, 512, 512, 3)
+    c = cos(out, ref)
+    assert c >= 0.999, c
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_sdxl_unet_reduced_depth_full_width(fp8):
+    """SDXL UNet widths (320/640/1280, head dim 64, 2048-d context, add-embeds) at reduced
+    transformer depth and a 32^2 latent, bf16 and OCP-fp8 attention, vs the fp32 reference"""
+    import dataclasses
+    from cassmantle_amd.models.unet import SDXL_UNET, UNet
+    cfg = dataclasses.replace(SDXL_UNET, transformer_depth=(0, 1, 1), mid_transformer_depth=1, sample_size=32)
+    m = UNet(cfg, seed=4).cuda()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(1, 32, 32, 4, generator=g).to(torch.bfloat16)
+    t = torch.tensor([500.0])
+    ctx = (torch.randn(1, 77, 2048, generator=g) * 0.5).to(torch.bfloat16)
+    added = {"time_ids": torch.tensor([[256.0, 256.0, 0.0, 0.0, 256.0, 256.0]]),
+             "text_embeds": (torch.randn(1, 1280, generator=g) * 0.5).to(torch.bfloat16)}
+    with torch.no_grad():
+        out = m(x.cuda(), t.cuda(), ctx.cuda(), {k: v.cuda() for k, v in added.items()}, fp8=fp8).float().cpu()
+        ref = _fp32_cpu_copy(m)(x.float(), t, ctx.float(), {k: v.float() for k, v in added.items()})
+    c = cos(out, ref)
+    assert c >= (0.995 if fp8 else 0.999), c
+
+
+def test_sd15_end_to_end_graph_vs_fp32_reference():
+    """a whole 4-step generation (CLIP encode -> graph-replayed denoise -> VAE decode -> uint8)
+    vs the same pipeline on the fp32 reference path: the images must agree, not just the shape"""
+    import numpy as np
     from cassmantle_amd.pipeline import SPECS, StableDiffusion
-    sd = StableDiffusion(SPECS["sd15"], device="cuda", use_graphs=True)
-    img = sd.generate_tensor(["A cubism style piece depicting the following: a lantern"], "blurry", [1], steps=4)
-    assert img.shape == (1, 512, 512, 3) and img.dtype == torch.uint8
+    sd = StableDiffusion(SPECS["sd15"], device="cuda", use_graphs=True, seed=0)
+    prompt = ["A cubism style piece depicting the following: a lantern"]
+    img = sd.generate(prompt, "blurry", [1], steps=4)[0]
+    ref_sd = StableDiffusion(SPECS["sd15"], device="cpu", use_graphs=False, seed=0, dtype=torch.float32)
+    with torch.no_grad():                    # identical (bf16-valued) weights, fp32 arithmetic
+        for a, b in [(sd.unet, ref_sd.unet), (sd.vae, ref_sd.vae)] + list(zip(sd.text_encoders, ref_sd.text_encoders)):
+            b.load_state_dict({k: v.float().cpu() for k, v in a.state_dict().items()})
+        ref_sd.unet.fuse_projections()
+    ref = ref_sd.generate(prompt, "blurry", [1], steps=4)[0]
+    assert img.shape == ref.shape == (512, 512, 3) and img.dtype == np.uint8
+    d = np.abs(img.astype(np.float32) - ref.astype(np.float32))
+    psnr = 10 * np.log10(255.0 ** 2 / max(float((d ** 2).mean()), 1e-9))
+    print(f"[e2e] psnr {psnr:.2f} dB, mean |diff| {d.mean():.3f}")
+    assert psnr > 28.0 and d.mean() < 6.0, (psnr, d.mean())
 
 
 def test_unet_is_bit_deterministic_run_to_run():
