@@ -51,7 +51,7 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
     p.stats = nullptr;
   }
   if (p.split > 1) {
-    auto ws = at::empty({(long long)p.split * p.M * p.N}, like.options().dtype(at::kFloat));
+    auto ws = at::empty({(long long)p.split * p.batch * p.M * p.N}, like.options().dtype(at::kFloat));
     launch_gemm(p, ws.data_ptr<float>(), cur_stream());
   } else {
     launch_gemm(p, nullptr, cur_stream());

@@ -18,6 +18,8 @@ void gemm_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_c3_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_pp_c0_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_pp_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
+bool gemm_areg_ok(const GemmArgs& p);
+void launch_gemm_areg(const GemmArgs& p, hipStream_t s);
 
 namespace {
 
@@ -31,9 +33,11 @@ constexpr int BK = 64;
 //   7: 256x256   8: 256x160   9: 256x128   10: 128x256
 // deep LDS ring (gemm_impl.h STAGES 4-5, one block per CU; buffer-resource modes, bf16 out):
 //   11: 128x160 4w S4   12: 128x128 4w S4 (also gated)   13: 128x64 4w S5   14: 128x160 8w S4
+//   15: A-in-registers short-K kernel (gemm_areg.hip: K = 320 / 640, W streamed in chunks)
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 15;
+constexpr int kNumTiles = 16;
+constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
 constexpr int kFirstDeep = 11;
 // slots = resident blocks on the chip: 128x64 needs 48 KiB of LDS per block, so 3 blocks fit a
@@ -43,7 +47,8 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 64, 0.80f, 768},  {256, 16, 0.25f, 512},  {256, 160, 1.02f, 256},
                                        {256, 128, 1.00f, 256}, {256, 256, 1.60f, 256}, {256, 160, 1.55f, 256},
                                        {256, 128, 1.45f, 256}, {128, 256, 1.45f, 256}, {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256}};
+                                       {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
+                                       {128, 64, 1.f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
@@ -177,7 +182,7 @@ void gemm_set_override(int cfg, int split) {
 static GemmPlan gemm_plan_impl(const GemmArgs& p);
 GemmPlan gemm_plan(const GemmArgs& p) {
   const GemmPlan r = gemm_plan_impl(p);
-  if (g_record_key) g_last_plan = r;
+  g_last_plan = r;
   return r;
 }
 
@@ -201,7 +206,8 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     }
     // a table entry is only taken if the kernel family can run this call (same checks as a
     // forced config), so a stale table never selects an unsupported path
-    if (have && (tp.cfg < kFirstPP || (tp.cfg < kFirstDeep ? pp_ok(p) : deep_ok(p)))) return tp;
+    const bool elig = tp.cfg < kFirstPP || (tp.cfg < kFirstDeep ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p) : deep_ok(p)));
+    if (have && elig) return tp;
   }
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
   const bool gated = p.act == ACT_GEGLU || p.act == ACT_SWIGLU;
@@ -212,7 +218,9 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   static const int pp_auto = env_int("CASSMANTLE_GEMM_PP", 0);
   const bool pp = pp_elig && pp_auto;
   const bool deep_elig = deep_ok(p);
-  if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
+  if (force_cfg == kAreg) {
+    if (gemm_areg_ok(p)) return GemmPlan{kAreg, 1};
+  } else if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
       (force_cfg < kFirstPP || (force_cfg < kFirstDeep ? pp_elig : deep_elig))) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
@@ -228,12 +236,14 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   }
   const int nk = (p.K + BK - 1) / BK;
   // M <= 8 goes to the GEMV path; short prompts (M = tens of rows) need split-K to fill the chip
-  const bool can_split = p.batch == 1 && p.N % 4 == 0 && p.K % 8 == 0 && p.M > 8;
+  // (batched calls -- the upsampling conv's 4 parity classes -- split per batch: slabs [z][split])
+  const bool can_split = p.N % 4 == 0 && p.K % 8 == 0 && p.M > 8;
   double best_t = 1e30;
   for (int c = 0; c < kNumTiles; ++c) {
     const TileCfg& tc = kTiles[c];
     if (only >= 0 ? c != only : ((c == 5 || c == 6) && !use_big)) continue;
     if (c >= kFirstDeep && only != c) continue;   // table / forced only
+    if (c == kAreg) continue;
     if (c >= kFirstPP && c < kFirstDeep && !(only >= 0 ? pp_elig : pp)) continue;
     if (c == 4 && p.N > 16) continue;
     if (c != 4 && p.N <= 16) continue;
@@ -249,7 +259,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
       // calibrated on MI355X: ~1.8 us per 128x128x64 k-tile per occupancy round (2 blocks/CU)
       double t = 1.8 * rounds * (kper + 2) * tile_cost * (waste > 1.3 ? waste : 1.0);
       // split-K: slab write + read at ~3 TB/s plus the extra reduce launch (~6 us in a graph)
-      if (split > 1) t += 6.0 + 2.0 * (double)split * p.M * p.N * 4 / 3.0e6;
+      if (split > 1) t += 6.0 + 2.0 * (double)split * p.batch * p.M * p.N * 4 / 3.0e6;
       if (only >= 0 && force_split > 0 && split != force_split) continue;
       if (t < best_t - 1e-9) { best_t = t; best = GemmPlan{c, split}; }
     }
@@ -275,6 +285,10 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     return;
   }
   const bool buf = buf_ok(p);
+  if (p.cfg == kAreg && gemm_areg_ok(p)) {
+    launch_gemm_areg(p, s);
+    return;
+  }
   if (p.cfg >= kFirstPP && p.cfg < kFirstDeep && pp_ok(p)) {
     if (!p.conv) gemm_pp_c0_launch(p, ws, s);
     else gemm_pp_c2_launch(p, ws, s);

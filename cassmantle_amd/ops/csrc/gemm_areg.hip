@@ -1,0 +1,319 @@
+// Short-K GEMM with the A operand held in REGISTERS (the UNet's level-1
+// transformer projections, QKV and GEGLU feed-forward, K = 320..640).
+//
+// Why a separate kernel: at K = 320 a tiled GEMM runs only 5 k-tiles per output tile, so every
+// tile pays its DMA prologue latency and its epilogue serially (measured 126 us for the
+// 32768 x 2560 x 320 GEGLU = 3.3 PF-equivalent 4.7x off its MFMA floor; profiles/
+// r2_autotune_sd15.jsonl).  Here a block owns BM = 128 rows and keeps their ENTIRE K extent as
+// MFMA B-operand fragments in VGPRs (each wave 32 rows: 2 x K/32 fragments, loaded once from
+// global memory), then streams the W matrix through a 2-3 deep LDS ring in chunks of BNC rows:
+// per chunk every wave runs K/32 x TI x 2 MFMAs against that chunk and writes its 32 x BNC
+// outputs straight from the accumulators (bias / GEGLU / residual / GroupNorm statistics
+// fused).  The next chunks' LDS-DMA overlaps the current chunk's MFMAs; the block never
+// returns to a prologue until all of its N range is done.
+//
+// Layout: D[n][m] = W[n][:] . A[m][:] as in gemm_impl.h (W rows on the MFMA row axis: each lane
+// owns 4 consecutive output columns of one row -> 8-byte stores).  W chunk LDS image: K/64
+// k-tiles of [BNC][64] bf16 (128-byte rows, chunk XOR-swizzled by (row >> 1) & 7 on the DMA
+// source address and the ds_read, conflict-free for the 16-row fragment reads).
+#include <stdlib.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+CM_DEVICE void areg_blds16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+CM_DEVICE void areg_wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+constexpr int AR_THREADS = 256;        // 4 waves, each owning 16 * RW rows
+
+// KS = K / 32 k-steps; TI = BNC / 16 W subtiles per chunk; RING = LDS chunk buffers;
+// RW = 16-row A fragments per wave (each W fragment read from LDS feeds RW MFMAs)
+template <int KS, int TI, int RING>
+constexpr int areg_minb() { return RING * 16 * TI * (KS / 2) * 128 <= 80 * 1024 ? 2 : 1; }
+
+template <int KS, int TI, int RING, int RW, bool GEGLU>
+__global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_areg_kernel(GemmArgs p, int chunks_per_block) {
+  constexpr int AR_BM = 64 * RW;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  constexpr int BNC = 16 * TI;                 // W rows per chunk
+  constexpr int KT = KS / 2;                   // 64-deep k-tiles
+  constexpr int CHUNK = BNC * KT * 8;          // uint4 per chunk buffer
+  constexpr int DMA_PER_CHUNK = (BNC * KT) / 32;   // 1 KiB pieces per wave (4 waves x 8 rows)
+  static_assert(KS % 2 == 0 && (BNC * KT) % 32 == 0, "whole DMA rounds");
+  static_assert(!GEGLU || TI % 2 == 0, "geglu value/gate pairs");
+  constexpr int OOB = (int)0x80000000;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int m0 = blockIdx.x * AR_BM + wave * 16 * RW;     // this wave's 16 * RW rows
+  const int nchunks = GEGLU ? (2 * p.N) / BNC : p.N / BNC;
+  const int c_begin = blockIdx.y * chunks_per_block;
+  const int c_end = min(nchunks, c_begin + chunks_per_block);
+  const int ldw = p.ldw ? p.ldw : p.K;
+
+  // ---- A fragments into registers: afr[j][ks] = 8 bf16 of row m0 + 16 j + fr, k = 32 ks + 8 fq
+  bf16x8_t afr[RW][KS];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int row = m0 + 16 * j + fr;
+    const bool ok = row < p.M;
+    const uint4* src = reinterpret_cast<const uint4*>(p.A + (long long)(ok ? row : 0) * p.lda) + fq;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 v = src[4 * ks];
+      if (!ok) v = make_uint4(0, 0, 0, 0);
+      afr[j][ks] = as_bf16x8(v);
+    }
+  }
+
+  // ---- W chunk staging: chunk c, LDS row (k-tile t, chunk row r) <- W row of (c, r), k 64 t..
+  __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.W), (short)0,
+                                                                  (int)(((long long)(p.Nw - 1) * ldw + p.K) * 2),
+                                                                  0x00020000);
+  // piece q of a chunk (q = 0 .. DMA_PER_CHUNK-1) covers LDS rows 32 q + 8 wave + (lane >> 3) of
+  // the [KT][BNC] row space; its lane moves chunk (lane & 7) ^ swz of that row
+  int w_vo_base[DMA_PER_CHUNK], w_koff[DMA_PER_CHUNK];
+  const int slot = lane & 7;
+#pragma unroll
+  for (int q = 0; q < DMA_PER_CHUNK; ++q) {
+    const int lr = 32 * q + 8 * wave + (lane >> 3);      // LDS row in the chunk image
+    const int t = lr / BNC, r = lr - t * BNC;             // k-tile, chunk row
+    const int ch = slot ^ ((r >> 1) & 7);
+    w_koff[q] = (t * 64 + ch * 8) * 2;                    // bytes within the W row
+    w_vo_base[q] = r;                                     // chunk row (W row resolved per chunk)
+  }
+  auto w_row_of = [&](int c, int r) -> int {              // W row for chunk c, chunk row r
+    if constexpr (GEGLU) {
+      // chunk c covers output columns [c * BNC/2, ...): 16-row blocks alternate value / gate
+      const int blk = r >> 4, within = r & 15;
+      const int nout = c * (BNC / 2) + (blk >> 1) * 16 + within;
+      return nout < p.N ? ((blk & 1) ? p.N + nout : nout) : -1;
+    } else {
+      const int n = c * BNC + r;
+      return n < p.Nw ? n : -1;
+    }
+  };
+  // every stage() issues exactly DMA_PER_CHUNK loads per wave (a chunk past the block's range
+  // moves zeros into a free buffer) so the vmcnt bookkeeping is static on every path
+  auto stage = [&](int c, int buf) {
+    uint4* base = smem + buf * CHUNK;
+    const bool live = c < c_end;
+#pragma unroll
+    for (int q = 0; q < DMA_PER_CHUNK; ++q) {
+      const int wr = live ? w_row_of(c, w_vo_base[q]) : -1;
+      const int vo = wr >= 0 ? (int)((long long)wr * ldw * 2 + w_koff[q]) : OOB;
+      areg_blds16(rsW, base + (32 * q + 8 * wave) * 8, vo, 0);
+    }
+  };
+
+  // fragment read offsets (uint4 units) within a chunk buffer: W subtile i rows 16 i + fr,
+  // k-step ks -> k-tile ks >> 1, logical 16-byte chunk 4 (ks & 1) + fq
+  auto w_off = [&](int i, int ks) {
+    const int r = 16 * i + fr;
+    return ((ks >> 1) * BNC + r) * 8 + ((4 * (ks & 1) + fq) ^ ((r >> 1) & 7));
+  };
+
+  const int hw = p.stats_hw > 0 ? p.stats_hw : 1;
+  static_assert(RING == 3, "one chunk in flight behind the one being retired");
+  stage(c_begin, 0);
+  stage(c_begin + 1, 1);
+
+  constexpr int NQ = GEGLU ? TI / 2 : TI;          // output column quads per row per chunk
+  for (int c = c_begin; c < c_end; ++c) {
+    const int rel = c - c_begin;
+    const int buf = rel % RING;
+    // retire chunk c (chunk c + 1 stays in flight), publish it.  After the first chunk this is
+    // already satisfied by the previous chunk's epilogue wait.
+    areg_wait_vmcnt<DMA_PER_CHUNK>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();            // chunk c landed; every wave is done with c-1's buffer
+
+    // epilogue operands of THIS chunk, loaded BEFORE the next DMA so that waiting for them
+    // (loads retire in order) leaves that DMA in flight
+    uint2 bq[NQ], gq[GEGLU ? NQ : 1], rq[RW][NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int n = GEGLU ? c * (BNC / 2) + 16 * i + 4 * fq : c * BNC + 16 * i + 4 * fq;
+      const bool nok = n < p.N;
+      bq[i] = make_uint2(0, 0);
+      if (GEGLU) gq[GEGLU ? i : 0] = make_uint2(0, 0);
+      if (p.bias && nok) {
+        bq[i] = *reinterpret_cast<const uint2*>(p.bias + n);
+        if (GEGLU) gq[GEGLU ? i : 0] = *reinterpret_cast<const uint2*>(p.bias + p.N + n);
+      }
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const int m = m0 + 16 * j + fr;
+        rq[j][i] = make_uint2(0, 0);
+        if (p.residual && nok && m < p.M) rq[j][i] = *reinterpret_cast<const uint2*>(p.residual + (long long)m * p.ldc + n);
+      }
+    }
+    stage(c + RING - 1, (rel + RING - 1) % RING);
+
+    const uint4* Bs = smem + buf * CHUNK;
+    f32x4_t acc[TI][RW];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < RW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // W fragments software-pipelined one k-step ahead of the MFMAs that consume them
+    bf16x8_t wf[2][TI];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) wf[0][i] = as_bf16x8(Bs[w_off(i, 0)]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) wf[(ks + 1) & 1][i] = as_bf16x8(Bs[w_off(i, ks + 1)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks & 1][i], afr[j][ks], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    areg_wait_vmcnt<DMA_PER_CHUNK>();   // this chunk's epilogue operands (and chunk c + 1) landed
+
+    // ---- epilogue straight from the accumulators: row m, columns n .. n+3
+    float ssum[TI][4], ssq[TI][4];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { ssum[i][e] = 0.f; ssq[i][e] = 0.f; }
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const int m = m0 + 16 * j + fr;
+      const bool mok = m < p.M;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int n = GEGLU ? c * (BNC / 2) + 16 * i + 4 * fq : c * BNC + 16 * i + 4 * fq;
+        if (!mok || n >= p.N) continue;
+        const float b[4] = {bf2f(bq[i].x & 0xffff), bf2f(bq[i].x >> 16), bf2f(bq[i].y & 0xffff), bf2f(bq[i].y >> 16)};
+        const float r[4] = {bf2f(rq[j][i].x & 0xffff), bf2f(rq[j][i].x >> 16), bf2f(rq[j][i].y & 0xffff),
+                            bf2f(rq[j][i].y >> 16)};
+        float o[4];
+        if constexpr (GEGLU) {
+          const uint2 g2 = gq[GEGLU ? i : 0];
+          const float gb[4] = {bf2f(g2.x & 0xffff), bf2f(g2.x >> 16), bf2f(g2.y & 0xffff), bf2f(g2.y >> 16)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gate_f(acc[2 * i][j][e] + b[e], acc[2 * i + 1][j][e] + gb[e], p.act) + r[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = acc[i][j][e] * p.alpha + b[e];
+          if (p.act != ACT_NONE) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = apply_act(o[e], p.act);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += r[e];
+        }
+        const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.C) + (long long)m * p.ldc + n) = pk;
+        if (!GEGLU && p.stats) {   // statistics of the STORED (bf16-rounded) values
+          const float q0 = bf2f(pk.x & 0xffff), q1 = bf2f(pk.x >> 16), q2 = bf2f(pk.y & 0xffff), q3 = bf2f(pk.y >> 16);
+          ssum[i][0] += q0; ssum[i][1] += q1; ssum[i][2] += q2; ssum[i][3] += q3;
+          ssq[i][0] = fmaf(q0, q0, ssq[i][0]); ssq[i][1] = fmaf(q1, q1, ssq[i][1]);
+          ssq[i][2] = fmaf(q2, q2, ssq[i][2]); ssq[i][3] = fmaf(q3, q3, ssq[i][3]);
+        }
+      }
+    }
+    if constexpr (!GEGLU) {
+      // GroupNorm statistics: a wave's 16 RW rows lie in one image (hw % 64 == 0, host-checked);
+      // reduce over the 16 row lanes sharing a column quad, one atomic per (column, stat)
+      if (p.stats && m0 < p.M) {
+        const int img = m0 / hw;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float a = ssum[i][e], b = ssq[i][e];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+            const int n = c * BNC + 16 * i + 4 * fq + e;
+            if (fr == 0 && n < p.N) {
+              stat_atomic_add(p.stats + ((long long)img * p.N + n) * 2 + 0, 0, a);
+              stat_atomic_add(p.stats + ((long long)img * p.N + n) * 2 + 1, 1, b);
+            }
+          }
+      }
+    }
+  }
+}
+
+template <int KS, int TI, int RING, int RW, bool GEGLU>
+void launch_areg_t(const GemmArgs& p, hipStream_t s) {
+  constexpr int AR_BM = 64 * RW;
+  constexpr int BNC = 16 * TI;
+  const int nchunks = GEGLU ? (2 * p.N) / BNC : p.N / BNC;
+  const int mblocks = (p.M + AR_BM - 1) / AR_BM;
+  // split the chunks over blocks until the grid covers the chip (each split re-loads its A rows
+  // into registers; they come from L2)
+  int groups = 1;
+  const int target = 256 * areg_minb<KS, TI, RING>();
+  while (mblocks * groups < target && nchunks / (groups * 2) >= 2) groups *= 2;
+  const int per = (nchunks + groups - 1) / groups;
+  const size_t lds = (size_t)RING * BNC * (KS / 2) * 128;
+  auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU>;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    once = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(mblocks, groups), dim3(AR_THREADS), lds, s, p, per);
+}
+
+}  // namespace
+
+// K = 320: 64-row chunks, 3-deep ring (120 KiB); K = 640: 32-row chunks, 3-deep ring (120 KiB)
+bool gemm_areg_ok(const GemmArgs& p) {
+  if (p.conv || p.A2 || p.batch != 1 || p.out_f32 || p.ln_rows || p.chan_bias || p.split > 1) return false;
+  if (!(p.K == 320 || p.K == 640) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
+  const bool gated = is_gated(p.act);
+  const int bnc = p.K == 320 ? 64 : 32;
+  if ((gated ? 2 * p.N : p.N) % bnc) return false;
+  if (gated && p.stats) return false;
+  if (p.stats && (p.stats_hw % 64 != 0)) return false;
+  // 16-byte A fragment loads, 8-byte bias / residual / output quads
+  if (((uintptr_t)p.A & 15) || ((uintptr_t)p.C & 7) || ((uintptr_t)p.residual & 7) || ((uintptr_t)p.bias & 7))
+    return false;
+  const long long lim = (1LL << 31) - 1;
+  return ((long long)(p.Nw - 1) * (p.ldw ? p.ldw : p.K) + p.K) * 2 <= lim;
+}
+
+static int areg_variant() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("CASSMANTLE_AREG_V");
+    v = e ? atoi(e) : -1;
+  }
+  return v;
+}
+
+// Instantiations (measured on the SD-1.5 batch-8 level-1/2 shapes, profiles/r2_areg_variants.jsonl):
+//   v0: 40 KiB chunks, 1 block / CU               v1: 20 KiB chunks, 2 blocks / CU
+//   v2: v1 with 64 rows per wave for gated K = 320 (each LDS W fragment feeds 4 MFMAs, not 2)
+// default (-1): v2 for the K = 320 GEGLU (127 -> 70 us), v1 otherwise
+void launch_gemm_areg(const GemmArgs& p, hipStream_t s) {
+  const bool gated = is_gated(p.act);
+  int v = areg_variant();
+  if (v < 0) v = 2;
+  if (p.K == 320) {
+    if (v == 2 && gated) launch_areg_t<10, 2, 3, 4, true>(p, s);   // RW = 4 spills without the gate pairing
+    else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true>(p, s) : launch_areg_t<10, 2, 3, 2, false>(p, s);
+    else gated ? launch_areg_t<10, 4, 3, 2, true>(p, s) : launch_areg_t<10, 4, 3, 2, false>(p, s);
+  } else {
+    if (gated) launch_areg_t<20, 2, 3, 2, true>(p, s);
+    else if (v >= 1) launch_areg_t<20, 1, 3, 2, false>(p, s);
+    else launch_areg_t<20, 2, 3, 2, false>(p, s);
+  }
+}

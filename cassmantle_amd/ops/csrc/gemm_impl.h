@@ -324,7 +324,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         for (int i = 0; i < TI; ++i) {
           const int n = n0 + wn * (BN / WN) + 16 * i + 4 * fq;
           if (m < p.M && n < p.N) {
-            float* dst = partial + ((long long)split_id * p.M + m) * p.N + n;
+            float* dst = partial + (((long long)batch * nsplit + split_id) * p.M + m) * p.N + n;
             *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
           }
         }
@@ -350,7 +350,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         if (n >= p.N) continue;
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (nsplit > 1) {               // split-K: raw fp32 partial slab
-          float* dst = partial + ((long long)split_id * p.M + m) * p.N + n;
+          float* dst = partial + (((long long)batch * nsplit + split_id) * p.M + m) * p.N + n;
           *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
         } else {
           epilogue4_call<OUTF32>(p, batch, m, n, acc[i][j]);
@@ -702,6 +702,9 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
 // block serially reading up to 15 slabs of its tile)
 template <bool OUTF32>
 __global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ partial, int split) {
+  // slabs of batch z (parity class of the upsampling conv) start at z * split * M * N
+  const int bz = blockIdx.y;
+  partial += (long long)bz * split * p.M * p.N;
   const long long nq = (long long)p.M * (p.N / 4);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long long)gridDim.x * blockDim.x) {
     const int m = (int)(i / (p.N / 4));
@@ -711,7 +714,7 @@ __global__ void splitk_reduce_kernel(GemmArgs p, const float* __restrict__ parti
       const float4 v = *reinterpret_cast<const float4*>(partial + ((long long)s * p.M + m) * p.N + n);
       o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
     }
-    epilogue4<OUTF32>(p, 0, m, n, o);
+    epilogue4<OUTF32>(p, bz, m, n, o);
   }
 }
 
@@ -729,6 +732,8 @@ template <bool OUTF32>
 __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, const float* __restrict__ partial,
                                                                   int split) {
   __shared__ float red[2][SK_RL][SK_QB * 4];
+  const int bz = blockIdx.z;
+  partial += (long long)bz * split * p.M * p.N;
   const int qd = threadIdx.x % SK_QB, rl = threadIdx.x / SK_QB;
   const int n = (blockIdx.x * SK_QB + qd) * 4;
   const int m0 = blockIdx.y * SK_RB;
@@ -768,7 +773,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
         const float4 v = *reinterpret_cast<const float4*>(src + sl * slab);
         o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
       }
-      epilogue4<OUTF32>(p, 0, m, n, o);      // (N % 8 == 0: o holds the final values)
+      epilogue4<OUTF32>(p, bz, m, n, o);     // (N % 8 == 0: o holds the final values)
       if (!single) {
         const int img = m / shw;
         if (img != cur) { flush(); cur = img; }
@@ -804,6 +809,20 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
   }
 }
 
+// the split-K second pass (slabs [batch][split][M][N] fp32)
+template <bool OUTF32>
+void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s) {
+  if (p.stats != nullptr) {
+    dim3 g2((unsigned)((p.N / 4 + SK_QB - 1) / SK_QB), (unsigned)((p.M + SK_RB - 1) / SK_RB), (unsigned)p.batch);
+    hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split);
+  } else {
+    const long long nq = (long long)p.M * (p.N / 4);
+    const long long nb = (nq + 255) / 256;
+    const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel<OUTF32>, dim3(rb, (unsigned)p.batch), dim3(256), 0, s, p, ws, split);
+  }
+}
+
 int g_stages_override = -1;   // CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark)
 
 int stages_pref() {
@@ -835,15 +854,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
     }
   }
   hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * WN), lds, s, p, ws);
-  if (split > 1 && p.stats != nullptr) {
-    dim3 g2((unsigned)((p.N / 4 + SK_QB - 1) / SK_QB), (unsigned)((p.M + SK_RB - 1) / SK_RB));
-    hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split);
-  } else if (split > 1) {
-    const long long nq = (long long)p.M * (p.N / 4);
-    const long long nb = (nq + 255) / 256;
-    const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel<OUTF32>, dim3(rb), dim3(256), 0, s, p, ws, split);
-  }
+  if (split > 1) launch_splitk_reduce<OUTF32>(p, ws, split, s);
 }
 
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, bool BUF>

@@ -386,15 +386,7 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
     once = true;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(512), lds, s, p, ws);
-  if (split > 1 && p.stats != nullptr) {
-    dim3 g2((unsigned)((p.N / 4 + SK_QB - 1) / SK_QB), (unsigned)((p.M + SK_RB - 1) / SK_RB));
-    hipLaunchKernelGGL(splitk_reduce_stats_kernel<false>, g2, dim3(256), 0, s, p, ws, split);
-  } else if (split > 1) {
-    const long long nq = (long long)p.M * (p.N / 4);
-    const long long nb = (nq + 255) / 256;
-    const unsigned rb = (unsigned)(nb < 2048 ? nb : 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(rb), dim3(256), 0, s, p, ws, split);
-  }
+  if (split > 1) launch_splitk_reduce<false>(p, ws, split, s);
 }
 
 // ping-pong tile menu (gemm.hip kPP* configs)

@@ -109,6 +109,28 @@ def test_conv_upsample_as_parity_2x2_convs(B, H, W, Cin, Cout):
     assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
 
 
+@pytest.mark.parametrize("cfg,split", [(1, 2), (1, 8), (0, 5), (8, 4)])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(8, 8, 8, 1280, 1280), (2, 6, 10, 64, 96)])
+def test_conv_upsample_parity_split_k(B, H, W, Cin, Cout, cfg, split, force_cfg):
+    """split-K on the batched (4 parity classes) upsampling conv: fp32 slabs [parity][split], the
+    reduce pass applies every epilogue input and the GroupNorm statistics per parity class"""
+    x = rnd(B, H, W, Cin, seed=85)
+    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=86)
+    b = rnd(Cout, scale=0.1, seed=87)
+    cb = rnd(B, Cout, scale=0.1, seed=88)
+    res = rnd(B, 2 * H, 2 * W, Cout, seed=89)
+    st = ops.new_stats(B, Cout, DEV)
+    force_cfg(cfg, split)
+    out = ops.conv2d_up2(x, w, None, b, residual=res, chan_bias=cb, stats=st)
+    exp = ref.conv2d(x, w, b, 1, 1, res, True, cb)
+    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
+    exp_st = ops.new_stats(B, Cout, DEV)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+    out2 = ops.conv2d_up2(x, w, None, b)
+    assert rel_err(out2, ref.conv2d(x, w, b, 1, 1, None, True, None)) < 1e-2
+
+
 def test_conv_epilogue_fusions():
     B, H, W, C = 2, 16, 16, 64
     x = rnd(B, H, W, C, seed=15)
@@ -417,6 +439,55 @@ def test_gemm_pp_geglu_cat_stats(cfg, force_cfg):
     out = ops.linear_cat(a, s2, w2, b2, stats=st)
     exp = ref.linear(torch.cat([a, s2], -1), w2, b2)
     assert rel_err(out, exp) < 1e-2
+    exp_st = ops.new_stats(B, N, DEV)
+    ops.channel_stats_ref(out, exp_st)
+    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
+
+
+# ---------------------------------------------------------------- A-in-registers short-K GEMM (cfg 15)
+@pytest.mark.parametrize("M,N,K", [(1000, 320, 320), (4096, 960, 320), (333, 640, 640), (4096, 1280, 640),
+                                   (77, 64, 320), (8192, 320, 640)])
+@pytest.mark.parametrize("act", ["none", "silu"])
+def test_gemm_areg_linear(M, N, K, act, force_cfg):
+    """gemm_areg.hip: partial last row block, N not a multiple of the chunk-group split, bias +
+    activation + residual, vs the fp32 reference; the planner must report cfg 15 actually ran"""
+    from cassmantle_amd.ops._ext import ext
+    x = rnd(M, K, seed=131)
+    w = rnd(N, K, scale=K ** -0.5, seed=132)
+    b = rnd(N, scale=0.1, seed=133)
+    r = rnd(M, N, seed=134)
+    force_cfg(15)
+    out = ops.linear(x, w, b, residual=r, act=act)
+    assert tuple(ext().gemm_last_plan())[0] == 15
+    assert rel_err(out, ref.linear(x, w, b, residual=r, act=act)) < 1e-2
+    out = ops.linear(x, w)
+    assert rel_err(out, ref.linear(x, w)) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(2000, 1280, 320), (1000, 2560, 640), (130, 32, 320)])
+def test_gemm_areg_geglu(M, N, K, force_cfg):
+    from cassmantle_amd.ops._ext import ext
+    x = rnd(M, K, seed=135)
+    w = rnd(2 * N, K, scale=K ** -0.5, seed=136)
+    b = rnd(2 * N, scale=0.1, seed=137)
+    force_cfg(15)
+    out = ops.linear(x, w, b, act="geglu")
+    assert tuple(ext().gemm_last_plan())[0] == 15
+    assert rel_err(out, ref.linear(x, w, b, act="geglu")) < 1e-2
+
+
+def test_gemm_areg_stats(force_cfg):
+    """fused GroupNorm statistics (per image: rows of one image are a multiple of 32)"""
+    from cassmantle_amd.ops._ext import ext
+    B, HW, K, N = 3, 320, 640, 640
+    x = rnd(B, HW, K, seed=138)
+    w = rnd(N, K, scale=K ** -0.5, seed=139)
+    b = rnd(N, scale=0.1, seed=140)
+    st = ops.new_stats(B, N, DEV)
+    force_cfg(15)
+    out = ops.linear(x, w, b, stats=st)
+    assert tuple(ext().gemm_last_plan())[0] == 15
+    assert rel_err(out, ref.linear(x, w, b)) < 1e-2
     exp_st = ops.new_stats(B, N, DEV)
     ops.channel_stats_ref(out, exp_st)
     assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
