@@ -494,7 +494,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional
             return o.transpose(1, 2)
         return ref.attention(q, k, v, scale, causal, kv_lens)
     B, Nq, H, _ = q.shape
-    if d > 160:
+    if d > 160 and d != 512:
         return _attention_gemm(q, k, v, scale, causal, kv_lens)
     out = torch.empty((B, Nq, H, d), device=q.device, dtype=q.dtype)
     # fp8 (head dim 64 only): the per-call K/V e4m3 pack costs more than the 2x-rate MFMAs save
@@ -506,8 +506,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional
 
 
 def _attention_gemm(q, k, v, scale, causal, kv_lens):
-    """Large head dim (VAE mid-block, d=512, single head): S = QK^T on MFMA GEMM, fused
-    row-softmax kernel, O = PV.  S fits HBM trivially ([B,4096,4096] fp32 = 64 MB/img)."""
+    """Large head dims other than 512 (d = 512, the VAE mid-block, runs the flash kernel of
+    attention_d512.hip): S = QK^T on MFMA GEMM, fused row-softmax kernel, O = PV; S is
+    materialised ([B, Nq, Nk] fp32), so this is a fallback, not a hot path."""
     B, Nq, H, d = q.shape
     outs = []
     for h in range(H):

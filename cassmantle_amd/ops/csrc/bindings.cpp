@@ -365,7 +365,7 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   a.o_sb = out.stride(0); a.o_sn = out.stride(1); a.o_sh = out.stride(2);
   a.B = (int)q.size(0); a.Nq = (int)q.size(1); a.H = (int)q.size(2); a.d = (int)q.size(3);
   a.Nk = (int)k.size(1);
-  TORCH_CHECK(a.d % 8 == 0 && a.d <= 160, "attention: head dim must be a multiple of 8 and <= 160");
+  TORCH_CHECK(a.d % 8 == 0 && (a.d <= 160 || a.d == 512), "attention: head dim must be a multiple of 8 and <= 160, or 512");
   TORCH_CHECK(k.size(2) == v.size(2) && a.H % k.size(2) == 0, "attention: query heads must be a multiple of kv heads");
   a.group = a.H / (int)k.size(2);
   for (long long st : {a.q_sb, a.q_sn, a.q_sh, a.k_sb, a.k_sn, a.k_sh, a.v_sb, a.v_sn, a.v_sh})
@@ -377,6 +377,13 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   if (kv_lens.has_value() && kv_lens->defined()) {
     TORCH_CHECK(kv_lens->scalar_type() == at::kInt && kv_lens->is_cuda(), "kv_lens must be int32 on device");
     a.kv_lens = kv_lens->data_ptr<int>();
+  }
+  if (a.d == 512) {
+    const long long wsb = attention_d512_workspace(a);
+    at::Tensor ws;
+    if (wsb > 0) ws = at::empty({wsb / 4}, q.options().dtype(at::kFloat));
+    launch_attention_d512(a, wsb > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+    return;
   }
   if (fp8 && a.d == 64) {
     // OCP e4m3 K/V packed per call (workspace from the caching allocator: graph-safe)

@@ -76,6 +76,10 @@ struct AttnArgs {
   int group = 1;                  // query heads per K/V head (GQA)
 };
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// head dim 512 (VAE mid-block): flash kernel; ws = attention_d512_workspace bytes (key-split
+// partials for short grids, 0 otherwise)
+long long attention_d512_workspace(const AttnArgs& a);
+void launch_attention_d512(const AttnArgs& a, float* ws, hipStream_t s);
 // fp8 (OCP e4m3) attention for head dim 64: ws = attention_fp8_workspace bytes (K8 + V8t)
 long long attention_fp8_workspace(const AttnArgs& a, int Hk);
 void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
