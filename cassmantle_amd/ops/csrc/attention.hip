@@ -38,7 +38,10 @@ struct AttnGeom {
 };
 
 template <int DQK, int DO, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
+// min blocks 8 / NW caps the kernel at 256 registers: the compiler then keeps the MFMA
+// accumulators in VGPRs, where the softmax reads and writes them (with a 512-register budget it
+// chose AGPRs and paid a v_accvgpr_read + write per score per pass: ~144 of ~300 VALU per tile)
+__global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2)) attn_fwd_kernel(AttnArgs a) {
   using G = AttnGeom<DQK, DO>;
   constexpr int THREADS = 64 * NW;
   constexpr int QB = 32 * NW;
@@ -405,7 +408,7 @@ __global__ void attn_fp8_pack_kernel(AttnArgs a, int Hk, int Nkp, uint8_t* __res
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
 template <int NW>
-__global__ void __launch_bounds__(64 * NW) attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8,
+__global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8,
                                                            const uint8_t* __restrict__ V8t) {
   constexpr int THREADS = 64 * NW;
   constexpr int QB = 32 * NW;

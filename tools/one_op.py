@@ -21,6 +21,10 @@ with torch.no_grad():
         B, N, H, d = [int(v) for v in sys.argv[2:6]]
         q, k, v = rnd(B, N, H, d), rnd(B, N, H, d), rnd(B, N, H, d)
         f = lambda: ops.attention(q, k, v)
+    elif kind == "attn8":
+        B, N, H, d = [int(v) for v in sys.argv[2:6]]
+        q, k, v = rnd(B, N, H, d), rnd(B, N, H, d), rnd(B, N, H, d)
+        f = lambda: ops.attention(q, k, v, fp8="force")
     for _ in range(iters):
         f()
     torch.cuda.synchronize()
