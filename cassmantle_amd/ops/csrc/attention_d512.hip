@@ -102,12 +102,17 @@ __global__ void __launch_bounds__(64 * NW5, 1) attn_d512_kernel(AttnArgs a, floa
     const int kb = k_begin + t * KT5;
     uint16_t* Kb = lds5 + (size_t)buf * TILEB;
     uint16_t* Vb = Kb + TILEB / 2;
+    // an opaque copy of the lane id: the per-row source offsets are recomputed per tile (2 VALU
+    // each) instead of being hoisted into registers, which spilled and put serial scratch
+    // reloads in front of every tile's DMA issue
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < KT5 / NW5; ++i) {
       const int r = wave + NW5 * i;                 // tile row (uniform)
       const int key = kb + r;
       const bool live = key < k_end;
-      const int kc = lane ^ (r & 15), vc = lane ^ (4 * (r & 3));
+      const int kc = ln ^ (r & 15), vc = ln ^ (4 * (r & 3));
       const int ko = live ? (int)((long long)key * a.k_sn * 2 + kc * 16) : OOB;
       const int vo = live ? (int)((long long)key * a.v_sn * 2 + vc * 16) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsK, (lds_void*)(Kb + r * D5), 16, ko, 0, 0, 0);
@@ -147,8 +152,12 @@ __global__ void __launch_bounds__(64 * NW5, 1) attn_d512_kernel(AttnArgs a, floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
     {
-      const char* krow = reinterpret_cast<const char*>(Kb + ql * D5);
-      const int sw = ql & 15;
+      // (opaque per-tile copies of the lane-dependent address terms: hoisted out of the loop they
+      // cost 16+ VGPRs and spilled; recomputed they are one v_xor per fragment read)
+      int qlv = ql;
+      asm volatile("" : "+v"(qlv));
+      const char* krow = reinterpret_cast<const char*>(Kb + qlv * D5);
+      const int sw = qlv & 15;
 #pragma unroll
       for (int ks = 0; ks < DH5 / 16; ++ks) {
         const int pc = (32 * dh + 2 * ks + hlf) ^ sw;
@@ -220,17 +229,24 @@ __global__ void __launch_bounds__(64 * NW5, 1) attn_d512_kernel(AttnArgs a, floa
     // 16 s + 8 (j >> 2) + 4 h + (j & 3))
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const char* vlo = reinterpret_cast<const char*>(Vb + (16 * s + tr_row) * D5) + tr_byte;
-      const char* vhi = vlo + 8 * ROWB;
+      int trr = tr_row;
+      asm volatile("" : "+v"(trr));
+      const char* vlo = reinterpret_cast<const char*>(Vb + (16 * s + trr) * D5) + tr_byte;
 #pragma unroll
-      for (int dc = 0; dc < DH5 / 32; ++dc) {
-        const int pc = ((4 * (8 * dh + dc) + tr_chunk) ^ tr_swz) * 16;
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(vlo + pc));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(vhi + pc));
-        typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-        const s16x8_t vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        oacc[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv), pf[s], oacc[dc], 0, 0, 0);
-        if ((dc & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      for (int g = 0; g < DH5 / 32; g += 4) {
+        // transposed reads + their wait in one asm statement (common.h ds_read_tr16_x4x2: the
+        // builtin made hipcc drain the next tile's in-flight DMA before every read)
+        uint32_t ad[4];
+        s16x4_t lo[4], hi[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ad[e] = lds_addr(vlo + ((4 * (8 * dh + g + e) + tr_chunk) ^ tr_swz) * 16);
+        ds_read_tr16_x4x2<8 * ROWB>(ad, lo, hi);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+          const s16x8_t vv = {lo[e][0], lo[e][1], lo[e][2], lo[e][3], hi[e][0], hi[e][1], hi[e][2], hi[e][3]};
+          oacc[g + e] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv), pf[s], oacc[g + e], 0, 0, 0);
+        }
       }
     }
   }

@@ -45,6 +45,35 @@ CM_DEVICE uint4 pack8(const float* f) {
 
 CM_DEVICE bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// Four pairs of ds_read_b64_tr_b16 (T10 hardware-transposed LDS reads) and their lgkmcnt(0) in
+// ONE asm statement (early-clobber outputs, so no output register is read, copied or reused
+// before the data lands: cdna_hip_programming.md §5.7 item 1 form (i)).  Pair e reads at lds
+// byte address a[e] and a[e] + HI_OFF.  hipcc's waitcnt pass treats the builtin form as aliasing
+// every LDS-DMA still in flight and emits s_waitcnt vmcnt(0) in front of it -- in a kernel that
+// keeps the next tile's buffer_load ... lds in flight that drains it every tile.
+template <int HI_OFF>
+CM_DEVICE void ds_read_tr16_x4x2(const uint32_t (&a)[4], s16x4_t (&lo)[4], s16x4_t (&hi)[4]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\t"
+      "ds_read_b64_tr_b16 %1, %8 offset:%c12\n\t"
+      "ds_read_b64_tr_b16 %2, %9\n\t"
+      "ds_read_b64_tr_b16 %3, %9 offset:%c12\n\t"
+      "ds_read_b64_tr_b16 %4, %10\n\t"
+      "ds_read_b64_tr_b16 %5, %10 offset:%c12\n\t"
+      "ds_read_b64_tr_b16 %6, %11\n\t"
+      "ds_read_b64_tr_b16 %7, %11 offset:%c12\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(lo[0]), "=&v"(hi[0]), "=&v"(lo[1]), "=&v"(hi[1]), "=&v"(lo[2]), "=&v"(hi[2]), "=&v"(lo[3]), "=&v"(hi[3])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "i"(HI_OFF)
+      : "memory");
+}
+CM_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <typename T>
+CM_DEVICE void lds_use(T& v) { asm volatile("" : "+v"(v)); }
+
 // SiLU / quick-GELU with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE divide:
 // the GroupNorm+SiLU apply and activation epilogues evaluate them per element
 CM_DEVICE float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }

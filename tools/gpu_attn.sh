@@ -8,4 +8,7 @@ rc=$?; tail -3 gpurun_out/attn_tests.log; echo "tests rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u tools/bench_attn.py ${ATTN_ARGS} > gpurun_out/attn_bench.jsonl 2> gpurun_out/attn_bench.err
 rc=$?; cat gpurun_out/attn_bench.jsonl; tail -3 gpurun_out/attn_bench.err; echo "bench rc=$rc"
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/bench_attn_d512.py > gpurun_out/a512_bench.jsonl 2> gpurun_out/a512_bench.err
+rc=$?; cat gpurun_out/a512_bench.jsonl; echo "d512 rc=$rc"
 exit $rc
