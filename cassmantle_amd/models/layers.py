@@ -209,6 +209,7 @@ class CrossAttention(nn.Module):
         self.to_out = Linear(dim, dim, bias=True, gen=gen, dtype=dtype)
 
     _kv = None   # view into the UNet's batched context-K/V buffer (set by UNet.set_context)
+    _kv8 = None  # its OCP-e4m3 image for the fp8 kernel (set by UNet.set_context(fp8=True))
 
     def forward(self, x, ctx, residual=None, fp8=False, q=None):
         """``q``: the query projection already computed (e.g. with a folded LayerNorm)."""
@@ -217,13 +218,16 @@ class CrossAttention(nn.Module):
         B, N = q.shape[0], q.shape[1]
         C = self.dim
         q = q.view(B, N, self.heads, self.head_dim)
+        kv8 = None
         if self._kv is not None and self._kv.shape[0] == B:
             # the text context is constant over the denoise loop: K/V of every cross-attention
-            # layer come from ONE GEMM per generation (strided views, no copies)
+            # layer come from ONE GEMM per generation (strided views, no copies), and with fp8
+            # their e4m3 image is packed once per generation too
             kv = self._kv.view(B, self._kv.shape[1], 2, self.heads, self.head_dim)
+            kv8 = self._kv8 if fp8 else None
         else:
             kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, self.heads, self.head_dim)
-        o = ops.attention(q, kv[:, :, 0], kv[:, :, 1], fp8=fp8)
+        o = ops.attention(q, kv[:, :, 0], kv[:, :, 1], fp8=fp8, kv8=kv8)
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
 

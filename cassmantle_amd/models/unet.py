@@ -290,15 +290,17 @@ class UNet(nn.Module):
         self._kv_bufs: dict = {}
         self._fused = True
 
-    def set_context(self, ctx: Optional[torch.Tensor]) -> None:
+    def set_context(self, ctx: Optional[torch.Tensor], fp8: bool = False) -> None:
         """Precompute all cross-attention K/V for a (constant) text context.  Buffers are kept
-        per shape and refilled in place, so a captured denoise graph sees the new context."""
+        per shape and refilled in place, so a captured denoise graph sees the new context.
+        ``fp8``: also pack each layer's K/V into the e4m3 image of the fp8 attention kernel."""
         if not getattr(self, "_fused", False):
             self.fuse_projections()
         ca = self.cross_attns()
         if ctx is None or self._kv_w is None:
             for m in ca:
                 m._kv = None
+                m._kv8 = None
             return
         kv = ops.linear(ctx, self._kv_w)                            # [B, L, sum 2C]
         key = tuple(kv.shape)
@@ -309,6 +311,12 @@ class UNet(nn.Module):
             buf.copy_(kv)
         for m in ca:
             m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
+            if fp8 and m.head_dim == 64 and ops._use_hip(buf):
+                kv = m._kv.view(buf.shape[0], buf.shape[1], 2, m.heads, m.head_dim)
+                old = m._kv8 if m._kv8 is not None and m._kv8.device == buf.device else None
+                m._kv8 = ops.pack_kv_fp8(kv[:, :, 0], kv[:, :, 1], out=old)
+            else:
+                m._kv8 = None
 
     def time_table(self, tsteps: torch.Tensor, nb: int, added: Optional[dict] = None):
         """Time conditioning of a whole denoise schedule at once: SiLU(temb) [E, nb, D] and every

@@ -472,11 +472,24 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
 
 
 # ----------------------------------------------------------------------------- attention (K1/K2/K3)
+def pack_kv_fp8(k: torch.Tensor, v: torch.Tensor, kv_lens: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """OCP-e4m3 K/V image of the fp8 attention kernel (K8 [B,Hk,Nkp,64] + V8t [B,Hk,64,Nkp]) as a
+    flat uint8 tensor; ``out`` (reused buffer, e.g. a captured graph's) is refilled in place.  The
+    cross-attention K/V are constant over a generation, so UNet.set_context packs them once."""
+    n = int(ext().attention_fp8_bytes(k.shape[0], k.shape[1], k.shape[2]))
+    if out is None or out.numel() != n:
+        out = torch.empty(n, device=k.device, dtype=torch.uint8)
+    ext().attention_fp8_pack(k, v, kv_lens, out)
+    return out
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,
               causal: bool = False, kv_lens: Optional[torch.Tensor] = None,
-              fp8: bool = False) -> torch.Tensor:
+              fp8: bool = False, kv8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Flash attention.  q [B,Nq,H,d], k/v [B,Nk,H,d]; strided views allowed (last dim
-    contiguous), e.g. slices of a fused QKV projection output.  Returns [B,Nq,H,d]."""
+    contiguous), e.g. slices of a fused QKV projection output.  Returns [B,Nq,H,d].
+    ``kv8``: K/V already packed by :func:`pack_kv_fp8` (fp8 path only)."""
     d = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(d)
     if not _use_hip(q):
@@ -497,12 +510,14 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional
     if d > 160 and d != 512:
         return _attention_gemm(q, k, v, scale, causal, kv_lens)
     out = torch.empty((B, Nq, H, d), device=q.device, dtype=q.dtype)
-    # fp8 (head dim 64 only): the per-call K/V e4m3 pack costs more than the 2x-rate MFMAs save
-    # below ~2k keys (measured: 1.08x at 4096 keys, 0.9x at 1024, 0.8x at 77), so short
-    # sequences keep the bf16 kernel unless fp8 == "force"
-    use8 = fp8 == "force" or (bool(fp8) and d == 64 and k.shape[1] >= 2048)
-    ext().attention(q, k, v, out, float(scale), int(causal), kv_lens, int(use8))
+    # fp8 (head dim 64 only): every self-attention (the per-call pack is one coalesced pass) and
+    # every cross-attention whose K/V were packed once per context (kv8)
+    use8 = fp8 == "force" or (bool(fp8) and d == 64 and (kv8 is not None or k.shape[1] >= FP8_MIN_KEYS))
+    ext().attention(q, k, v, out, float(scale), int(causal), kv_lens, int(use8), kv8 if use8 else None)
     return out
+
+
+FP8_MIN_KEYS = 256   # below this a per-call pack is not amortised (77-token cross-attention packs once)
 
 
 def _attention_gemm(q, k, v, scale, causal, kv_lens):

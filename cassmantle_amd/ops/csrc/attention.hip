@@ -368,41 +368,45 @@ CM_DEVICE int f8_slot(int kk) {
   return 32 * h + 16 * hf + r;
 }
 
-__global__ void attn_fp8_pack_kernel(AttnArgs a, int Hk, int Nkp, uint8_t* __restrict__ K8,
-                                     uint8_t* __restrict__ V8t) {
-  // thread = (b, kv head, 8-wide d chunk, key); keys fastest so V8t byte rows are coalesced
-  const long long total = (long long)a.B * Hk * 8 * Nkp;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int key = (int)(i % Nkp);
-  long long r = i / Nkp;
-  const int ch = (int)(r % 8);
-  r /= 8;
-  const int hh = (int)(r % Hk);
-  const int b = (int)(r / Hk);
-  uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+// one block per (64-key tile, kv head, batch): K rows convert straight to K8 (8 B per thread,
+// 64-B rows); V goes through a 64 x 64-byte LDS image in the V8t slot order and leaves as
+// 64-byte d-rows (16 B per thread).  The round-1 version wrote V8t one BYTE per store (13.4 us
+// for 2 x 4096 x 10 heads; profiles/r2_attn_fp8_kernel_trace.txt)
+__global__ void __launch_bounds__(256) attn_fp8_pack_kernel(AttnArgs a, int Hk, int Nkp, uint8_t* __restrict__ K8,
+                                                            uint8_t* __restrict__ V8t) {
+  __shared__ __attribute__((aligned(16))) uint8_t vt[64][64 + 16];
+  const int kb = blockIdx.x * 64, hh = blockIdx.y, b = blockIdx.z;
   int nk = a.Nk;
   if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
-  if (key < nk && ch * 8 < a.d) {
-    kv = *reinterpret_cast<const uint4*>(a.k + (long long)b * a.k_sb + (long long)key * a.k_sn +
-                                         (long long)hh * a.k_sh + ch * 8);
-    vv = *reinterpret_cast<const uint4*>(a.v + (long long)b * a.v_sb + (long long)key * a.v_sn +
-                                         (long long)hh * a.v_sh + ch * 8);
-  }
-  float kf[8], vf[8];
-  unpack8(kv, kf);
-  unpack8(vv, vf);
   const long long bh = (long long)b * Hk + hh;
-  *reinterpret_cast<uint2*>(K8 + (bh * Nkp + key) * 64 + ch * 8) =
-      make_uint2(f8x4(kf[0], kf[1], kf[2], kf[3]), f8x4(kf[4], kf[5], kf[6], kf[7]));
-  const uint32_t v0 = f8x4(vf[0], vf[1], vf[2], vf[3]), v1 = f8x4(vf[4], vf[5], vf[6], vf[7]);
-  const int slot = (key & ~63) + f8_slot(key & 63);
-  uint8_t* vt = V8t + (bh * 64 + ch * 8) * Nkp + slot;
+  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)hh * a.k_sh;
+  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)hh * a.v_sh;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    vt[(long long)e * Nkp] = (uint8_t)(v0 >> (8 * e));
-    vt[(long long)(e + 4) * Nkp] = (uint8_t)(v1 >> (8 * e));
+  for (int it = 0; it < 2; ++it) {
+    const int c = threadIdx.x + 256 * it;          // 512 chunks = 64 keys x 8 chunks of 8 d
+    const int kk = c >> 3, ch = c & 7;
+    const int key = kb + kk;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (key < nk && ch * 8 < a.d) {
+      kv = *reinterpret_cast<const uint4*>(Kp + (long long)key * a.k_sn + ch * 8);
+      vv = *reinterpret_cast<const uint4*>(Vp + (long long)key * a.v_sn + ch * 8);
+    }
+    float kf[8], vf[8];
+    unpack8(kv, kf);
+    unpack8(vv, vf);
+    *reinterpret_cast<uint2*>(K8 + (bh * Nkp + key) * 64 + ch * 8) =
+        make_uint2(f8x4(kf[0], kf[1], kf[2], kf[3]), f8x4(kf[4], kf[5], kf[6], kf[7]));
+    const uint32_t v0 = f8x4(vf[0], vf[1], vf[2], vf[3]), v1 = f8x4(vf[4], vf[5], vf[6], vf[7]);
+    const int slot = f8_slot(kk);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      vt[ch * 8 + e][slot] = (uint8_t)(v0 >> (8 * e));
+      vt[ch * 8 + e + 4][slot] = (uint8_t)(v1 >> (8 * e));
+    }
   }
+  __syncthreads();
+  const int dr = threadIdx.x >> 2, seg = threadIdx.x & 3;
+  *reinterpret_cast<uint4*>(V8t + (bh * 64 + dr) * Nkp + kb + seg * 16) = *reinterpret_cast<const uint4*>(&vt[dr][seg * 16]);
 }
 
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
@@ -584,12 +588,17 @@ long long attention_fp8_workspace(const AttnArgs& a, int Hk) {
   return 2LL * a.B * Hk * Nkp * 64;   // bytes: K8 + V8t
 }
 
-void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s) {
+void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s) {
+  const int Nkp = (a.Nk + KT - 1) / KT * KT;
+  hipLaunchKernelGGL(attn_fp8_pack_kernel, dim3((unsigned)(Nkp / 64), (unsigned)Hk, (unsigned)a.B), dim3(256), 0, s, a, Hk,
+                     Nkp, ws, ws + (long long)a.B * Hk * Nkp * 64);
+}
+
+void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed) {
   const int Nkp = (a.Nk + KT - 1) / KT * KT;
   uint8_t* K8 = ws;
   uint8_t* V8t = ws + (long long)a.B * Hk * Nkp * 64;
-  const long long total = (long long)a.B * Hk * 8 * Nkp;
-  hipLaunchKernelGGL(attn_fp8_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, Hk, Nkp, K8, V8t);
+  if (!packed) launch_attention_fp8_pack(a, Hk, ws, s);
   const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
   if (blocks8 >= 1024) {
     const int nqb = (a.Nq + 255) / 256;

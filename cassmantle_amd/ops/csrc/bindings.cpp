@@ -351,8 +351,8 @@ void embed_layer_norm(const at::Tensor& word, const at::Tensor& ids, const at::T
                           cur_stream());
 }
 
-void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, double scale,
-               int64_t causal, const c10::optional<at::Tensor>& kv_lens, int64_t fp8) {
+static AttnArgs attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, double scale,
+                          int64_t causal, const c10::optional<at::Tensor>& kv_lens) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
   TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4 && out.dim() == 4, "attention: [B,N,H,d] tensors");
   TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1 && out.stride(3) == 1,
@@ -378,6 +378,29 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
     TORCH_CHECK(kv_lens->scalar_type() == at::kInt && kv_lens->is_cuda(), "kv_lens must be int32 on device");
     a.kv_lens = kv_lens->data_ptr<int>();
   }
+  return a;
+}
+
+// K8 / V8t bytes of an fp8 attention over these K/V (B x kv heads x keys rounded to 64 x 64 x 2)
+int64_t attention_fp8_bytes(int64_t B, int64_t Nk, int64_t Hk) { return 2 * B * Hk * ((Nk + 63) / 64 * 64) * 64; }
+
+// pack K/V [B, Nk, Hk, 64] (any strides, last dim contiguous) into kv8 once -- the cross-attention
+// K/V are constant over a whole generation (UNet.set_context)
+void attention_fp8_pack(const at::Tensor& k, const at::Tensor& v, const c10::optional<at::Tensor>& kv_lens,
+                        at::Tensor& kv8) {
+  at::Tensor out = at::empty({1, 1, 1, k.size(3)}, k.options());
+  AttnArgs a = attn_args(k, k, v, out, 1.0, 0, kv_lens);
+  TORCH_CHECK(a.d == 64, "fp8 attention: head dim 64 only");
+  const int Hk = (int)k.size(2);
+  TORCH_CHECK(kv8.is_cuda() && kv8.scalar_type() == at::kByte && kv8.is_contiguous() &&
+                  kv8.numel() == attention_fp8_bytes(a.B, a.Nk, Hk), "kv8: contiguous uint8 of attention_fp8_bytes");
+  launch_attention_fp8_pack(a, Hk, kv8.data_ptr<uint8_t>(), cur_stream());
+}
+
+void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, double scale,
+               int64_t causal, const c10::optional<at::Tensor>& kv_lens, int64_t fp8,
+               const c10::optional<at::Tensor>& kv8) {
+  AttnArgs a = attn_args(q, k, v, out, scale, causal, kv_lens);
   if (a.d == 512) {
     const long long wsb = attention_d512_workspace(a);
     at::Tensor ws;
@@ -386,8 +409,14 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
     return;
   }
   if (fp8 && a.d == 64) {
-    // OCP e4m3 K/V packed per call (workspace from the caching allocator: graph-safe)
     const int Hk = (int)k.size(2);
+    if (kv8.has_value() && kv8->defined()) {          // K/V packed earlier (cross-attention)
+      TORCH_CHECK(kv8->is_cuda() && kv8->scalar_type() == at::kByte &&
+                      kv8->numel() == attention_fp8_bytes(a.B, a.Nk, Hk), "kv8 does not match K/V");
+      launch_attention_fp8(a, Hk, kv8->data_ptr<uint8_t>(), cur_stream(), true);
+      return;
+    }
+    // OCP e4m3 K/V packed per call (workspace from the caching allocator: graph-safe)
     auto ws = at::empty({attention_fp8_workspace(a, Hk)}, q.options().dtype(at::kByte));
     launch_attention_fp8(a, Hk, ws.data_ptr<uint8_t>(), cur_stream());
     return;
@@ -588,6 +617,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("group_norm_stats", &group_norm_stats);
   m.def("channel_stats", &channel_stats);
   m.def("attention", &attention);
+  m.def("attention_fp8_pack", &attention_fp8_pack);
+  m.def("attention_fp8_bytes", &attention_fp8_bytes);
   m.def("gather_cosine", &gather_cosine);
   m.def("pair_cosine", &pair_cosine);
   m.def("cosine_gemv", &cosine_gemv);

@@ -82,7 +82,10 @@ long long attention_d512_workspace(const AttnArgs& a);
 void launch_attention_d512(const AttnArgs& a, float* ws, hipStream_t s);
 // fp8 (OCP e4m3) attention for head dim 64: ws = attention_fp8_workspace bytes (K8 + V8t)
 long long attention_fp8_workspace(const AttnArgs& a, int Hk);
-void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
+// packed = true: ws already holds K8/V8t of these K/V (attention_fp8_pack once per text
+// context for cross-attention), only the attention kernel runs
+void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed = false);
+void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
 
 // norms
 void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,

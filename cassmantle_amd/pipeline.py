@@ -204,7 +204,7 @@ class StableDiffusion:
         st = self._state(B, ctx, plan, added)
         # cross-attention K/V of the (loop-invariant) text context: one GEMM per generation,
         # written into per-shape buffers that the captured step graph reads
-        self.unet.set_context(ctx)
+        self.unet.set_context(ctx, fp8=self.fp8)
         # time embedding + every ResNet's time bias for all timesteps of the plan: one batched
         # MLP + GEMM per generation (in place, so a captured step graph reads the new values)
         st.load_time(*self.unet.time_table(st.tsteps, st.unet_in.shape[0], added))

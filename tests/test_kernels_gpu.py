@@ -349,6 +349,41 @@ def test_attention_fp8(B, Nq, Nk, H, causal, lens):
     assert torch.isfinite(out8.float()).all()
 
 
+@pytest.mark.parametrize("B,Nq,Nk,H,lens", [(2, 4096, 77, 10, None), (2, 1024, 77, 20, None),
+                                          (3, 200, 130, 2, [130, 65, 3])])
+def test_attention_fp8_prepacked_kv(B, Nq, Nk, H, lens):
+    """cross-attention fp8: K/V packed ONCE (ops.pack_kv_fp8, as UNet.set_context does) and
+    reused; must equal the per-call-pack result bit for bit, through fused-KV strides"""
+    d = 64
+    q = rnd(B, Nq, H, d, scale=2.0, seed=44)
+    kv = rnd(B, Nk, 2, H, d, seed=45)
+    kl = torch.tensor(lens, dtype=torch.int32, device=DEV) if lens else None
+    k, v = kv[:, :, 0], kv[:, :, 1]
+    kv8 = ops.pack_kv_fp8(k, v, kl)
+    out_pre = ops.attention(q, k, v, kv_lens=kl, fp8=True, kv8=kv8)
+    out_call = ops.attention(q, k, v, kv_lens=kl, fp8="force")
+    assert torch.equal(out_pre, out_call)
+    assert rel_err(out_pre, ref.attention(q, k, v, kv_lens=kl)) < 0.12
+    kv8b = ops.pack_kv_fp8(k, v, kl, out=kv8)            # refill in place (captured graphs)
+    assert kv8b.data_ptr() == kv8.data_ptr()
+
+
+def test_unet_set_context_fp8_packs_cross_kv():
+    import dataclasses
+    from cassmantle_amd.models.unet import SDXL_UNET, UNet
+    cfg = dataclasses.replace(SDXL_UNET, transformer_depth=(0, 1, 1), mid_transformer_depth=1, sample_size=16)
+    m = UNet(cfg, seed=6).cuda()
+    ctx = rnd(2, 77, 2048, scale=0.5, seed=46)
+    m.set_context(ctx, fp8=True)
+    ca = m.cross_attns()
+    assert ca and all(c._kv8 is not None for c in ca)
+    ptrs = [c._kv8.data_ptr() for c in ca]
+    m.set_context(rnd(2, 77, 2048, scale=0.5, seed=47), fp8=True)
+    assert [c._kv8.data_ptr() for c in ca] == ptrs     # refilled in place
+    m.set_context(ctx, fp8=False)
+    assert all(c._kv8 is None for c in ca)
+
+
 def test_attention_softmax_spike():
     # force the online-softmax rescale: one key dominates late in the sequence
     B, N, H, d = 1, 512, 2, 64
