@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--no-score", action="store_true")
     p.add_argument("--fp8-attention", action="store_true")
+    p.add_argument("--overlap", action="store_true", help="VAE decode on a side stream, overlapped with the next step's denoise")
+    p.add_argument("--no-batch1", action="store_true", help="skip the batch-1 latency (s/image one room waits)")
     p.add_argument("--profile-steps", type=int, default=0)
     return p.parse_args()
 
@@ -120,7 +122,7 @@ def main() -> int:
     args.denoise_steps = args.denoise_steps or spec.steps
     args.scheduler = args.scheduler or spec.scheduler
     sd = StableDiffusion(spec, device=device, use_graphs=not (args.baseline or args.no_graphs),
-                         fp8_attention=args.fp8_attention, seed=0)
+                         fp8_attention=args.fp8_attention, seed=0, overlap_decode=args.overlap)
     gen = SyntheticPromptGenerator(salt=rank)
     seeds_txt, styles = load_seeds(), load_styles()
     negative = "blurry, distorted, fake, abstract, negative"
@@ -142,8 +144,15 @@ def main() -> int:
         nonlocal gather_buf
         prompts = room_prompts(step)
         seeds = [1000 * rank + 10 * step + j for j in range(args.batch)]
-        img = sd.generate_tensor(prompts, negative, seeds, steps=args.denoise_steps, scheduler=args.scheduler)
+        # sync_caller=False: the next step's encode + denoise start while this step's VAE decode
+        # still runs on the pipeline's decode stream (stage overlap); the timed region still
+        # ends with a device-wide synchronize
+        img = sd.generate_tensor(prompts, negative, seeds, steps=args.denoise_steps, scheduler=args.scheduler,
+                                 sync_caller=False)
         if world > 1:
+            cur = torch.cuda.current_stream(device)
+            cur.wait_stream(sd.out_stream)
+            img.record_stream(cur)
             if gather_buf is None:
                 gather_buf = [torch.empty_like(img) for _ in range(world)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -184,6 +193,18 @@ def main() -> int:
         dist.all_gather(allv, mine_t)
         per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "all_gather_ms": round(float(v[1]), 3)}
                     for i, v in enumerate(allv)]
+    # batch-1 latency: one room's single image end to end (prompt -> uint8 on host), what a
+    # serving room waits on; one warm-up generation (graph capture for batch 1), then 2 timed
+    b1 = None
+    if not args.no_batch1 and device.type == "cuda":
+        p1 = room_prompts(10_000)[:1]
+        sd.generate(p1, negative, [7], steps=args.denoise_steps, scheduler=args.scheduler)
+        lat1 = []
+        for i in range(2):
+            t1 = time.perf_counter()
+            sd.generate(p1, negative, [8 + i], steps=args.denoise_steps, scheduler=args.scheduler)
+            lat1.append(time.perf_counter() - t1)
+        b1 = round(float(np.median(lat1)), 4)
     # finiteness of the final LATENTS (the uint8 image is finite by construction)
     finite = bool(sd.last_finite.item()) if sd.last_finite is not None else None
 
@@ -221,6 +242,8 @@ def main() -> int:
             "graphs": bool(sd.use_graphs),
             "finite": finite,
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
+            "batch1_s_per_image": b1,       # one room, one image, prompt -> host uint8
+            "stage_overlap": sd.decode_stream is not None,
             "stage_mean_ms": stage_ms,      # device time per generation (incl. warmup)
             **score,
         }

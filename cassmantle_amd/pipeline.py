@@ -116,7 +116,7 @@ class _StepState:
 
 class StableDiffusion:
     def __init__(self, spec: PipelineSpec, device=None, dtype=torch.bfloat16, seed: int = 0,
-                 use_graphs: bool = True, fp8_attention: bool = False) -> None:
+                 use_graphs: bool = True, fp8_attention: bool = False, overlap_decode: bool = False) -> None:
         self.spec = spec
         self.device = torch.device(device) if device is not None else default_device()
         self.dtype = dtype
@@ -131,6 +131,14 @@ class StableDiffusion:
         # generation runs on its own stream (never the legacy default stream), so a serving
         # process can overlap it with the scorer's high-priority stream (BASELINE config 5)
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # stage overlap (opt-in): the VAE decode of generation i runs on its own stream,
+        # concurrently with the encode + denoise of generation i+1 (the latents it reads are a
+        # bf16 copy, so the next denoise may overwrite the step state at once).  Measured OFF by
+        # default: 605 vs 599 ms per 4-image step on MI355X, same box interleaved x2
+        # (profiles/r2_stage_overlap_ab.txt) -- the decode's kernels slow the concurrent graph
+        # replay by more than the 21 ms of encode + decode they hide
+        self.decode_stream = (torch.cuda.Stream(device=self.device)
+                              if self.device.type == "cuda" and overlap_decode else None)
         # one generation at a time per pipeline: the per-shape step state (latents, K/V context
         # buffers, time table, captured graph) is shared, so concurrent callers (several rooms'
         # worker threads) must not interleave (serving batches rooms through
@@ -260,11 +268,21 @@ class StableDiffusion:
                 x0 = self.init_latents(seeds, plan)
             with span("denoise", self.stream):
                 x = self.denoise(ctx, x0, plan, added)
-            with span("decode", self.stream):
-                self.last_finite = torch.isfinite(x).all()
-                img = self.vae.decode_uint8(x.to(self.dtype))
+            self.last_finite = torch.isfinite(x).all()
+            z = x.to(self.dtype)
+            if self.decode_stream is None:
+                with span("decode", self.stream):
+                    img = self.vae.decode_uint8(z)
+        out_stream = self.stream
+        if self.decode_stream is not None:
+            self.decode_stream.wait_stream(self.stream)
+            with torch.cuda.stream(self.decode_stream), span("decode", self.decode_stream):
+                z.record_stream(self.decode_stream)
+                img = self.vae.decode_uint8(z)
+            out_stream = self.decode_stream
+        self.out_stream = out_stream
         if caller is not None and sync_caller:
-            caller.wait_stream(self.stream)
+            caller.wait_stream(out_stream)
             img.record_stream(caller)
         return img
 
@@ -273,14 +291,15 @@ class StableDiffusion:
             img = self.generate_tensor(prompts, negative, seeds, sync_caller=False, **kw)
             finite = self.last_finite
             if self.stream is not None:
-                # D2H on the generation stream itself and a wait on THAT stream only: nothing is
-                # enqueued on the caller thread's (possibly legacy default) stream
-                with torch.cuda.stream(self.stream):
+                # D2H on the stream that produced the image and a wait on THAT stream only:
+                # nothing is enqueued on the caller thread's (possibly legacy default) stream
+                out = self.out_stream
+                with torch.cuda.stream(out):
                     host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
                     host.copy_(img, non_blocking=True)
                     ok = torch.empty((), dtype=torch.bool, pin_memory=True)
                     ok.copy_(finite, non_blocking=True)
-                self.stream.synchronize()
+                out.synchronize()
                 arr, fin = host.numpy(), bool(ok)
             else:
                 arr, fin = img.numpy(), bool(finite)

@@ -210,3 +210,18 @@ def test_legacy_stream_scorer_not_blocked_by_generation():
     assert gens[0] >= 1
     # one 12-step generation of 2 images takes ~100 ms: queueing behind it would put p50 there
     assert len(lat) > 200 and float(np.percentile(lat, 50)) < 20.0, (len(lat), np.percentile(lat, 50))
+
+
+def test_stage_overlap_decode_matches_serial():
+    """stage overlap: generation i's VAE decode runs on the decode stream while generation i+1
+    denoises; back-to-back un-synchronised calls must still give exactly the serial images"""
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    a = StableDiffusion(SPECS["sd15"], device="cuda", seed=0, overlap_decode=True)
+    b = StableDiffusion(SPECS["sd15"], device="cuda", seed=0, overlap_decode=False)
+    prompts = [["a lantern", "a river"], ["an ember", "a tower"], ["a shadow", "a forest"]]
+    outs = [a.generate_tensor(p, "blurry", [i, i + 10], steps=6, sync_caller=False) for i, p in enumerate(prompts)]
+    torch.cuda.synchronize()
+    ref = [b.generate_tensor(p, "blurry", [i, i + 10], steps=6) for i, p in enumerate(prompts)]
+    torch.cuda.synchronize()
+    for x, y in zip(outs, ref):
+        assert torch.equal(x, y)
