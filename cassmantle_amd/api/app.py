@@ -18,6 +18,8 @@ route              method  behaviour (reference cite)
 Additions (not part of the public contract): ``?room=<id>`` on every route selects a room
 (default room ``""`` = the reference's single global round); ``/metrics`` (Prometheus text,
 off unless ``metrics_enabled``); ``/healthz``.
+``GET /spell?word=w`` -> ``{"word","ok","suggestions"}``: the affix spell check + suggestions
+of the client (static/spell.js, reference Typo.js check/suggest) on the server (game/spell.py).
 """
 from __future__ import annotations
 
@@ -126,6 +128,17 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         finally:
             if session_id:
                 room.remove_connection(session_id)
+
+    @app.get("/spell")
+    async def spell(request: Request, word: str = ""):
+        """server twin of the client's affix spell check (game/spell.py == static/spell.js)"""
+        if (r := limited(request, "/spell", gcfg.rate_game)) is not None:
+            return r
+        from ..game.spell import spell_report
+        w = word.strip()[:32]
+        if not w.isalpha():
+            return JSONResponse({"word": w, "ok": False, "suggestions": []})
+        return JSONResponse(await asyncio.to_thread(spell_report, w, 5))
 
     @app.get("/client/status")
     async def check_status(request: Request, session_id: Optional[str] = Cookie(None)):

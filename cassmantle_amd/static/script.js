@@ -11,16 +11,16 @@ const params = new URLSearchParams(window.location.search);
 const ROOM = params.get("room");
 const q = (path) => (ROOM ? `${path}${path.includes("?") ? "&" : "?"}room=${encodeURIComponent(ROOM)}` : path);
 
-let dictionary = null;           // Set of lower-case words (/data/words.txt)
+let dictionary = null;           // AffixSpeller (static/spell.js) over /data/words.{aff,dic}
 let clockSocket = null;
 
 async function loadDictionary() {
   try {
-    const res = await fetch("/data/words.txt");
-    const text = await res.text();
-    dictionary = new Set(text.split("\n").map((w) => w.trim()).filter(Boolean));
+    const [aff, dic] = await Promise.all([fetch("/data/words.aff").then((r) => r.text()),
+                                          fetch("/data/words.dic").then((r) => r.text())]);
+    dictionary = new AffixSpeller(aff, dic);
   } catch (e) {
-    dictionary = null;  // spell-check disabled if the list is unavailable
+    dictionary = null;  // spell-check disabled if the dictionary is unavailable
   }
 }
 
@@ -121,8 +121,27 @@ function flashRed(el) {
 
 function validGuess(v) {
   if (!v || /\s/.test(v) || /[^A-Za-z'-]/.test(v)) return false;
-  if (dictionary && !dictionary.has(v.toLowerCase())) return false;
+  if (dictionary && !dictionary.check(v)) return false;
   return true;
+}
+
+// typo hint under the guess boxes: "did you mean ...?" (click a suggestion to take it)
+function showSuggestions(inp) {
+  const box = $("suggest");
+  if (!box) return;
+  box.textContent = "";
+  const v = inp.value.trim();
+  if (!dictionary || !v || /[^A-Za-z]/.test(v)) return;
+  const sug = dictionary.suggest(v, 3);
+  if (!sug.length) return;
+  box.append(`"${v}" is not in the dictionary. Did you mean `);
+  sug.forEach((w, i) => {
+    const a = document.createElement("a");
+    a.href = "#";
+    a.textContent = w;
+    a.addEventListener("click", (e) => { e.preventDefault(); inp.value = w; box.textContent = ""; });
+    box.append(a, i + 1 < sug.length ? ", " : "?");
+  });
 }
 
 async function submitGuesses() {
@@ -131,7 +150,7 @@ async function submitGuesses() {
   let ok = true;
   for (const inp of inputs) {
     const v = inp.value.trim();
-    if (!validGuess(v)) { flashRed(inp); ok = false; continue; }
+    if (!validGuess(v)) { flashRed(inp); showSuggestions(inp); ok = false; continue; }
     payload[inp.dataset.index] = v;
   }
   if (!ok || Object.keys(payload).length === 0) return;

@@ -174,3 +174,17 @@ def test_round_boundary_prewarms_blur_cache_1024():
         hits = cache.hits
         img = base64.b64decode(client.get("/fetch/contents").json()["image"])
         assert img[:2] == b"\xff\xd8" and cache.hits == hits + 1
+
+
+def test_media_assets_served():
+    """procedurally generated media (tools/make_media.py) stand in for the reference's media/"""
+    client, _ = make_client()
+    with client:
+        png = client.get("/media/background.png")
+        assert png.status_code == 200 and png.content[:8] == b"\x89PNG\r\n\x1a\n"
+        ico = client.get("/media/icon.ico")
+        assert ico.status_code == 200 and ico.content[:4] == b"\x00\x00\x01\x00"
+        for name in ("person-circle.svg", "code-mark.svg", "logo.svg"):
+            assert client.get(f"/media/{name}").status_code == 200
+        page = client.get("/").text
+        assert "/static/spell.js" in page and "/media/icon.ico" in page
