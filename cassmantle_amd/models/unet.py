@@ -105,7 +105,7 @@ class ResnetBlock(nn.Module):
 # LayerNorm folded into the following projection GEMM (row-statistics pass + epilogue
 # correction).  Measured neutral on SD-1.5 (684 vs 681 ms/step, profiles/r1_bench_lnfold_ab.jsonl):
 # the read-only statistics pass costs about what the LayerNorm kernel did, so it is opt-in.
-_LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "0") == "1"
+_LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "1") == "1"
 
 
 class BasicTransformerBlock(nn.Module):

@@ -64,7 +64,7 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
 void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act,
           const c10::optional<at::Tensor>& stats, int64_t stats_hw,
-          const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum) {
+          const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum, double ln_eps) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
@@ -101,6 +101,23 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     TORCH_CHECK(!p.out_f32 || p.act == 0, "gemm: folded LayerNorm with fp32 output supports no activation");
     p.ln_rows = ln_rows->data_ptr<float>();
     p.ln_wsum = ln_wsum->data_ptr<float>();
+  } else if (ln_wsum.has_value() && ln_wsum->defined() && ln_eps > 0) {
+    // folded LayerNorm with the row statistics computed where they are cheapest: inside the
+    // A-in-registers kernel when it takes the shape (K = 320 / 640), else a row-stats pass
+    CHECK_DEV(*ln_wsum); CHECK_CONTIG(*ln_wsum);
+    TORCH_CHECK(ln_wsum->scalar_type() == at::kFloat && ln_wsum->numel() == p.Nw, "gemm: ln_wsum fp32 [Nw]");
+    TORCH_CHECK(p.M > 8 && p.K % 8 == 0 && p.lda % 8 == 0 && !p.out_f32, "gemm: folded LayerNorm needs the MFMA path");
+    p.ln_wsum = ln_wsum->data_ptr<float>();
+    p.ln_eps = (float)ln_eps;
+    if (!gemm_areg_ok(p)) {
+      TORCH_CHECK(x.is_contiguous() && p.K <= 4096, "gemm: folded LayerNorm row statistics need contiguous rows");
+      at::Tensor rows = at::empty({p.M, 2}, x.options().dtype(at::kFloat));
+      launch_row_stats(bptr(x), rows.data_ptr<float>(), p.M, p.K, (float)ln_eps, cur_stream());
+      p.ln_rows = rows.data_ptr<float>();
+      p.ln_eps = 0.f;
+      run_gemm(p, out);
+      return;
+    }
   }
   run_gemm(p, out);
 }
@@ -596,7 +613,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("out"),
         py::arg("act"), py::arg("stats"), py::arg("stats_hw"), py::arg("ln_rows") = py::none(),
-        py::arg("ln_wsum") = py::none());
+        py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0);
   m.def("row_stats", &row_stats);
   m.def("gemm_cat", &gemm_cat);
   m.def("group_norm_cat", &group_norm_cat);

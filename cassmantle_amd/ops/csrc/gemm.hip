@@ -18,8 +18,6 @@ void gemm_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_c3_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_pp_c0_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void gemm_pp_c2_launch(const GemmArgs& p, float* ws, hipStream_t s);
-bool gemm_areg_ok(const GemmArgs& p);
-void launch_gemm_areg(const GemmArgs& p, hipStream_t s);
 
 namespace {
 
@@ -142,7 +140,7 @@ std::string gemm_key(const GemmArgs& p) {
   snprintf(buf, sizeof(buf), "m%d n%d k%d w%d b%d c%d:%d:%d:%d:%d:%d:%d:%d p%d a%d g%d s%d r%d cb%d ln%d f%d",
            p.M, p.N, p.K, p.Nw, p.batch, p.conv, p.IH, p.IW, p.Cin, p.stride, p.ksize, p.pad, p.upsample, p.parity,
            p.A2 != nullptr, is_gated(p.act) ? 1 : 0, p.stats != nullptr, p.residual != nullptr, p.chan_bias != nullptr,
-           p.ln_rows != nullptr, p.out_f32);
+           p.ln_rows != nullptr ? 1 : (p.ln_wsum != nullptr ? 2 : 0), p.out_f32);
   return std::string(buf);
 }
 
@@ -194,6 +192,9 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   }
   const int force_cfg = g_force_cfg, force_split = g_force_split;
   if (g_record_key) g_last_key = gemm_key(p);
+  // in-kernel LayerNorm statistics exist only in the A-in-registers kernel (the binding checked
+  // eligibility, so neither the table nor a forced config may pick anything else)
+  if (p.ln_wsum != nullptr && p.ln_rows == nullptr) return GemmPlan{kAreg, 1};
   if (force_cfg < 0) {
     bool have = false;
     GemmPlan tp{0, 1};

@@ -39,7 +39,10 @@ constexpr int AR_THREADS = 256;        // 4 waves, each owning 16 * RW rows
 template <int KS, int TI, int RING>
 constexpr int areg_minb() { return RING * 16 * TI * (KS / 2) * 128 <= 80 * 1024 ? 2 : 1; }
 
-template <int KS, int TI, int RING, int RW, bool GEGLU>
+// LNK: LayerNorm folded into the GEMM with the row statistics computed here, from the A rows
+// already resident in registers (W = W * gamma, bias = bias + W . beta; epilogue
+// rstd * (acc - mean * wsum[n]) -- no LayerNorm kernel, no normalised copy, no stats pass)
+template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
 __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_areg_kernel(GemmArgs p, int chunks_per_block) {
   constexpr int AR_BM = 64 * RW;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -72,6 +75,35 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
       uint4 v = src[4 * ks];
       if (!ok) v = make_uint4(0, 0, 0, 0);
       afr[j][ks] = as_bf16x8(v);
+    }
+  }
+  // ---- LayerNorm row statistics: a row's K values sit in the 4 lanes fr, fr+16, fr+32, fr+48
+  float ln_mean[RW], ln_rstd[RW];
+  if constexpr (LNK) {
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      // one pass (sum, sum of squares): a second pass re-unpacked the same fragments and the
+      // compiler kept all K/4 unpacked floats live between the passes (spills)
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 u = __builtin_bit_cast(uint4, afr[j][ks]);
+        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = __uint_as_float(w4[e] << 16), hi = __uint_as_float(w4[e] & 0xffff0000u);
+          s1 += lo + hi;
+          s2 = fmaf(lo, lo, fmaf(hi, hi, s2));
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      const float mu = s1 * (1.f / (32 * KS));
+      s2 = fmaxf(s2 * (1.f / (32 * KS)) - mu * mu, 0.f) * (32 * KS);
+      ln_mean[j] = mu;
+      ln_rstd[j] = rsqrtf(s2 * (1.f / (32 * KS)) + p.ln_eps);
     }
   }
 
@@ -140,6 +172,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
     // epilogue operands of THIS chunk, loaded BEFORE the next DMA so that waiting for them
     // (loads retire in order) leaves that DMA in flight
     uint2 bq[NQ], gq[GEGLU ? NQ : 1], rq[RW][NQ];
+    float4 wv[LNK ? NQ : 1], wg[LNK && GEGLU ? NQ : 1];   // folded-LayerNorm column sums
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int n = GEGLU ? c * (BNC / 2) + 16 * i + 4 * fq : c * BNC + 16 * i + 4 * fq;
@@ -149,6 +182,10 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
       if (p.bias && nok) {
         bq[i] = *reinterpret_cast<const uint2*>(p.bias + n);
         if (GEGLU) gq[GEGLU ? i : 0] = *reinterpret_cast<const uint2*>(p.bias + p.N + n);
+      }
+      if constexpr (LNK) {
+        wv[i] = nok ? *reinterpret_cast<const float4*>(p.ln_wsum + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (GEGLU) wg[i] = nok ? *reinterpret_cast<const float4*>(p.ln_wsum + p.N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int j = 0; j < RW; ++j) {
@@ -205,11 +242,27 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
         if constexpr (GEGLU) {
           const uint2 g2 = gq[GEGLU ? i : 0];
           const float gb[4] = {bf2f(g2.x & 0xffff), bf2f(g2.x >> 16), bf2f(g2.y & 0xffff), bf2f(g2.y >> 16)};
+          float hv[4] = {acc[2 * i][j][0], acc[2 * i][j][1], acc[2 * i][j][2], acc[2 * i][j][3]};
+          float gv[4] = {acc[2 * i + 1][j][0], acc[2 * i + 1][j][1], acc[2 * i + 1][j][2], acc[2 * i + 1][j][3]};
+          if constexpr (LNK) {
+            const float wh[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w}, wgg[4] = {wg[i].x, wg[i].y, wg[i].z, wg[i].w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = gate_f(acc[2 * i][j][e] + b[e], acc[2 * i + 1][j][e] + gb[e], p.act) + r[e];
+            for (int e = 0; e < 4; ++e) {
+              hv[e] = ln_rstd[j] * fmaf(-ln_mean[j], wh[e], hv[e]);
+              gv[e] = ln_rstd[j] * fmaf(-ln_mean[j], wgg[e], gv[e]);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gate_f(hv[e] + b[e], gv[e] + gb[e], p.act) + r[e];
         } else {
+          if constexpr (LNK) {
+            const float wh[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = acc[i][j][e] * p.alpha + b[e];
+            for (int e = 0; e < 4; ++e) o[e] = ln_rstd[j] * fmaf(-ln_mean[j], wh[e], acc[i][j][e]) + b[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = acc[i][j][e] * p.alpha + b[e];
+          }
           if (p.act != ACT_NONE) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = apply_act(o[e], p.act);
@@ -250,7 +303,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
   }
 }
 
-template <int KS, int TI, int RING, int RW, bool GEGLU>
+template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
 void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   constexpr int AR_BM = 64 * RW;
   constexpr int BNC = 16 * TI;
@@ -263,7 +316,7 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   while (mblocks * groups < target && nchunks / (groups * 2) >= 2) groups *= 2;
   const int per = (nchunks + groups - 1) / groups;
   const size_t lds = (size_t)RING * BNC * (KS / 2) * 128;
-  auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU>;
+  auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU, LNK>;
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -277,6 +330,7 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
 // K = 320: 64-row chunks, 3-deep ring (120 KiB); K = 640: 32-row chunks, 3-deep ring (120 KiB)
 bool gemm_areg_ok(const GemmArgs& p) {
   if (p.conv || p.A2 || p.batch != 1 || p.out_f32 || p.ln_rows || p.chan_bias || p.split > 1) return false;
+  if (p.ln_wsum && !(p.ln_eps > 0.f)) return false;
   if (!(p.K == 320 || p.K == 640) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
   const bool gated = is_gated(p.act);
   const int bnc = p.K == 320 ? 64 : 32;
@@ -303,17 +357,27 @@ static int areg_variant() {
 //   v0: 40 KiB chunks, 1 block / CU               v1: 20 KiB chunks, 2 blocks / CU
 //   v2: v1 with 64 rows per wave for gated K = 320 (each LDS W fragment feeds 4 MFMAs, not 2)
 // default (-1): v2 for the K = 320 GEGLU (127 -> 70 us), v1 otherwise
-void launch_gemm_areg(const GemmArgs& p, hipStream_t s) {
+template <bool LNK>
+void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   const bool gated = is_gated(p.act);
   int v = areg_variant();
   if (v < 0) v = 2;
-  if (p.K == 320) {
-    if (v == 2 && gated) launch_areg_t<10, 2, 3, 4, true>(p, s);   // RW = 4 spills without the gate pairing
-    else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true>(p, s) : launch_areg_t<10, 2, 3, 2, false>(p, s);
-    else gated ? launch_areg_t<10, 4, 3, 2, true>(p, s) : launch_areg_t<10, 4, 3, 2, false>(p, s);
-  } else {
-    if (gated) launch_areg_t<20, 2, 3, 2, true>(p, s);
-    else if (v >= 1) launch_areg_t<20, 1, 3, 2, false>(p, s);
-    else launch_areg_t<20, 2, 3, 2, false>(p, s);
+  if (LNK && v == 2) v = 1;      // the 64-rows-per-wave GEGLU tile has no registers left for the stats
+  if constexpr (LNK) {
+    if (v == 2) v = 1;
   }
+  if (p.K == 320) {
+    if (!LNK && v == 2 && gated) launch_areg_t<10, 2, 3, 4, true, false>(p, s);   // RW = 4 spills without the gate pairing
+    else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
+    else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
+  } else {
+    if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
+    else if (v >= 1) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
+    else launch_areg_t<20, 2, 3, 2, false, LNK>(p, s);
+  }
+}
+
+void launch_gemm_areg(const GemmArgs& p, hipStream_t s) {
+  if (p.ln_wsum != nullptr) launch_gemm_areg_t<true>(p, s);
+  else launch_gemm_areg_t<false>(p, s);
 }

@@ -39,6 +39,9 @@ struct GemmArgs {
   // float2, ln_wsum [Nw] fp32 column sums of the folded W
   const float* ln_rows = nullptr;
   const float* ln_wsum = nullptr;
+  // ln_wsum set, ln_rows null, ln_eps > 0: the row statistics are computed INSIDE the kernel from
+  // the register-resident A rows (A-in-registers short-K GEMM, gemm_areg.hip, only)
+  float ln_eps = 0.f;
   // GroupNorm statistics of the output: atomically accumulated per-(image, column) sum and
   // sum-of-squares [M / stats_hw][N][2] int64 fixed point (common.h; zeroed by the caller);
   // stats_hw = rows per image
@@ -104,6 +107,9 @@ long long group_norm_workspace(int B, long long S, int C);
 void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t* beta, uint16_t* y,
                        long long rows, int D, float eps, hipStream_t s);
 // per-row (mean, rstd) float2 of [rows][D] (LayerNorm statistics for a folded-LN GEMM)
+// A-in-registers short-K GEMM (gemm_areg.hip): shapes it takes, and the launch
+bool gemm_areg_ok(const GemmArgs& p);
+void launch_gemm_areg(const GemmArgs& p, hipStream_t s);
 void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s);
 // fused encoder input layer: y[r] = LN(word[ids[r]] + pos[r % seq] + add) (bf16, D % 8 == 0)
 void launch_embed_layer_norm(const uint16_t* word, const long long* ids, const uint16_t* pos, int seq,

@@ -253,6 +253,28 @@ def test_layer_norm_folded_into_gemm(rows, K, N, act, res):
     assert rel_err(out, exp) < 1.5e-2
 
 
+@pytest.mark.parametrize("rows,K,N,act,res", [(32768, 320, 960, None, False), (1000, 320, 320, None, True),
+                                              (2000, 320, 1280, "geglu", False), (8192, 640, 1920, None, False),
+                                              (333, 640, 2560, "geglu", True), (500, 640, 640, "silu", True)])
+def test_layer_norm_stats_inside_areg_gemm(rows, K, N, act, res):
+    """K = 320 / 640: the folded LayerNorm's row statistics come from the A rows resident in the
+    A-in-registers kernel (no stats pass); the plan must be cfg 15 and the result the explicit
+    LayerNorm -> GEMM reference"""
+    from cassmantle_amd.ops._ext import ext
+    x = rnd(rows, K, seed=76) * 1.5 + 0.3
+    g = rnd(K, seed=77) * 0.3 + 1
+    be = rnd(K, seed=78) * 0.2
+    Nw = 2 * N if act == "geglu" else N
+    w = rnd(Nw, K, scale=K ** -0.5, seed=79)
+    b = rnd(Nw, scale=0.1, seed=80)
+    r = rnd(rows, N, seed=81) if res else None
+    fold = ops.ln_fold(g, be, w, b)
+    out = ops.ln_linear(x, g, be, 1e-5, w, b, residual=r, act=act, fold=fold)
+    assert tuple(ext().gemm_last_plan())[0] == 15
+    exp = ref.linear(ref.layer_norm(x, g, be, 1e-5), w, b, residual=r, act=act)
+    assert rel_err(out, exp) < 1.5e-2
+
+
 @pytest.mark.parametrize("D,rows", [(320, 333), (384, 333), (768, 333), (1280, 333), (32, 333), (640, 1),
                                     (4096, 7), (136, 45)])
 def test_layer_norm(D, rows):
