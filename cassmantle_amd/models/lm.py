@@ -32,6 +32,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..utils.tracing import TRACER
 
 
 @dataclass(frozen=True)
