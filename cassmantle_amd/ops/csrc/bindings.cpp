@@ -609,14 +609,20 @@ void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
 
 }  // namespace
 
+using nogil = py::call_guard<py::gil_scoped_release>;
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cassmantle_amd gfx950 (CDNA4) HIP kernel library";
+  // Every launcher runs without the GIL: a kernel launch can block while the device queue is
+  // full behind a long generation (hundreds of eager VAE / encoder launches after a denoise
+  // graph), and holding the GIL there froze the scorer thread of a serving process for the
+  // whole wait (~110 ms spikes in test_legacy_stream_scorer_not_blocked_by_generation).
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("out"),
         py::arg("act"), py::arg("stats"), py::arg("stats_hw"), py::arg("ln_rows") = py::none(),
-        py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0);
-  m.def("row_stats", &row_stats);
-  m.def("gemm_cat", &gemm_cat);
-  m.def("group_norm_cat", &group_norm_cat);
+        py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0, nogil());
+  m.def("row_stats", &row_stats, nogil());
+  m.def("gemm_cat", &gemm_cat, nogil());
+  m.def("group_norm_cat", &group_norm_cat, nogil());
   m.def("gemm_set_override", [](int64_t cfg, int64_t split) { gemm_set_override((int)cfg, (int)split); });
   m.def("gemm_tune_set", [](const std::string& key, int64_t cfg, int64_t split) { gemm_tune_set(key, (int)cfg, (int)split); });
   m.def("gemm_tune_clear", []() { gemm_tune_clear(); });
@@ -624,30 +630,30 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_record_keys", [](bool on) { gemm_record_keys(on); });
   m.def("gemm_last_key", []() { return gemm_last_key(); });
   m.def("gemm_last_plan", []() { int c, sp; gemm_last_plan(&c, &sp); return std::vector<int64_t>{c, sp}; });
-  m.def("gemm_rms", &gemm_rms);
-  m.def("conv2d", &conv2d);
-  m.def("conv2d_up2", &conv2d_up2);
-  m.def("bmm_nt", &bmm_nt);
-  m.def("group_norm", &group_norm);
-  m.def("layer_norm", &layer_norm);
-  m.def("embed_layer_norm", &embed_layer_norm);
-  m.def("group_norm_stats", &group_norm_stats);
-  m.def("channel_stats", &channel_stats);
-  m.def("attention", &attention);
-  m.def("attention_fp8_pack", &attention_fp8_pack);
-  m.def("attention_fp8_bytes", &attention_fp8_bytes);
-  m.def("gather_cosine", &gather_cosine);
-  m.def("pair_cosine", &pair_cosine);
-  m.def("cosine_gemv", &cosine_gemv);
-  m.def("mean_pool_l2", &mean_pool_l2);
-  m.def("gaussian_blur", &gaussian_blur);
-  m.def("to_uint8", &to_uint8);
-  m.def("timestep_embedding", &timestep_embedding);
-  m.def("latent_step", &latent_step);
-  m.def("advance_step", &advance_step);
-  m.def("softmax_rows", &softmax_rows);
-  m.def("rms_norm", &rms_norm);
-  m.def("rope_kv", &rope_kv);
-  m.def("decode_attention", &decode_attention);
+  m.def("gemm_rms", &gemm_rms, nogil());
+  m.def("conv2d", &conv2d, nogil());
+  m.def("conv2d_up2", &conv2d_up2, nogil());
+  m.def("bmm_nt", &bmm_nt, nogil());
+  m.def("group_norm", &group_norm, nogil());
+  m.def("layer_norm", &layer_norm, nogil());
+  m.def("embed_layer_norm", &embed_layer_norm, nogil());
+  m.def("group_norm_stats", &group_norm_stats, nogil());
+  m.def("channel_stats", &channel_stats, nogil());
+  m.def("attention", &attention, nogil());
+  m.def("attention_fp8_pack", &attention_fp8_pack, nogil());
+  m.def("attention_fp8_bytes", &attention_fp8_bytes, nogil());
+  m.def("gather_cosine", &gather_cosine, nogil());
+  m.def("pair_cosine", &pair_cosine, nogil());
+  m.def("cosine_gemv", &cosine_gemv, nogil());
+  m.def("mean_pool_l2", &mean_pool_l2, nogil());
+  m.def("gaussian_blur", &gaussian_blur, nogil());
+  m.def("to_uint8", &to_uint8, nogil());
+  m.def("timestep_embedding", &timestep_embedding, nogil());
+  m.def("latent_step", &latent_step, nogil());
+  m.def("advance_step", &advance_step, nogil());
+  m.def("softmax_rows", &softmax_rows, nogil());
+  m.def("rms_norm", &rms_norm, nogil());
+  m.def("rope_kv", &rope_kv, nogil());
+  m.def("decode_attention", &decode_attention, nogil());
   m.attr("arch") = "gfx950";
 }

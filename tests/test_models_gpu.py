@@ -209,7 +209,8 @@ def test_legacy_stream_scorer_not_blocked_by_generation():
     th.join(timeout=60)
     assert gens[0] >= 1
     # one 12-step generation of 2 images takes ~100 ms: queueing behind it would put p50 there
-    assert len(lat) > 200 and float(np.percentile(lat, 50)) < 20.0, (len(lat), np.percentile(lat, 50))
+    assert len(lat) > 100 and float(np.percentile(lat, 50)) < 20.0, (len(lat), np.percentile(lat, 50))
+    print(f"[legacy-stream scorer] {len(lat)} calls, p50 {np.percentile(lat, 50):.2f} ms, p90 {np.percentile(lat, 90):.2f} ms")
 
 
 def test_stage_overlap_decode_matches_serial():
