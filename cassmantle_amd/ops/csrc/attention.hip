@@ -108,6 +108,10 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   // row sum of P comes out of the P.V MFMAs (rescaled with O for free) instead of 32 VALU adds
   // and a cross-half shuffle per tile
   constexpr bool ones = DO > DQK;   // d <= DQK < DO: at least one zero-padded V column
+  // head dim 40 (QK^T over 48): the first padding column also carries the running max, so
+  // S - m comes out of the MFMA -- K[:, 40] = 1 and Q^T[40][q] = -m (bf16, kept exact by
+  // tracking m as a bf16 value): no per-score accumulator initialisation
+  constexpr bool MF = (DQK == 48 && DO == 64);
 
   // staging geometry is tile-invariant: decode (key, chunk) once per thread; per tile only the
   // uniform key base moves (the first version re-derived it per tile: ~40 VALU per tile)
@@ -115,13 +119,14 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   int k_key[KLD], v_key[VLD], k_lds[KLD], v_lds[VLD];
   const uint16_t* k_src[KLD];
   const uint16_t* v_src[VLD];
-  bool k_use[KLD], v_use[VLD], v_one[VLD];
+  bool k_use[KLD], v_use[VLD], v_one[VLD], k_one[KLD];
 #pragma unroll
   for (int i = 0; i < KLD; ++i) {
     const int idx = tid + i * THREADS;
     const int key = idx / G::KCH, ch = idx - key * G::KCH;
     k_key[i] = key;
     k_use[i] = key < KT && ch * 8 < d;
+    k_one[i] = MF && key < KT && ch * 8 == d;     // K[:, d] = 1.0 -> the -m column of Q^T
     k_lds[i] = key < KT ? key * G::KSTR + ch * 8 : -1;
     k_src[i] = Kp + (long long)key * a.k_sn + ch * 8;
   }
@@ -140,7 +145,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
 #pragma unroll
     for (int i = 0; i < KLD; ++i) {
-      uint4 v = make_uint4(0, 0, 0, 0);
+      uint4 v = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
       if (k_use[i] && kbase + k_key[i] < nk) v = *reinterpret_cast<const uint4*>(k_src[i] + ko);
       kr[i] = v;
     }
@@ -180,7 +185,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[hf][r] = -m_run;   // S - m folded into the MFMA accumulator
+      for (int r = 0; r < 16; ++r) sacc[hf][r] = MF ? 0.f : -m_run;   // S - m folded into the MFMA
       const uint16_t* krow = Ks + (hf * 32 + ql) * G::KSTR + 8 * hlf;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
@@ -216,10 +221,22 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (t == 0 || !__all(mx <= RESCALE_THR)) {
+    if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
+      // a real branch: without the volatile asm hipcc if-converts this block and rescales O
+      // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
+      asm volatile("" ::: "memory");
       float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
       if (!(delta > -1e30f)) delta = 0.f;            // fully masked tile for this query
-      m_run += delta;
+      if constexpr (MF) {
+        // the new reference max as a bf16 value (it is an MFMA operand); only the rounded
+        // shift is applied, so every quantity stays consistent
+        const float mn = (float)(__bf16)(m_run + delta);
+        delta = mn - m_run;
+        m_run = mn;
+        qf[2][0] = hlf ? (__bf16)(-m_run) : qf[2][0];
+      } else {
+        m_run += delta;
+      }
       const float alpha = __builtin_amdgcn_exp2f(-delta);
       l_run *= alpha;
 #pragma unroll
@@ -518,7 +535,10 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (t == 0 || !__all(mx <= RESCALE_THR)) {
+    if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
+      // a real branch: without the volatile asm hipcc if-converts this block and rescales O
+      // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
+      asm volatile("" ::: "memory");
       float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
       if (!(delta > -1e30f)) delta = 0.f;
       m_run += delta;

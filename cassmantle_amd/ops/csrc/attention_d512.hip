@@ -192,7 +192,10 @@ __global__ void __launch_bounds__(64 * NW5, 1) attn_d512_kernel(AttnArgs a, floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (t == 0 || !__all(mx <= RESCALE_THR)) {
+    if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
+      // a real branch: without the volatile asm hipcc if-converts this block and rescales O
+      // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
+      asm volatile("" ::: "memory");
       float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
       if (!(delta > -1e30f)) delta = 0.f;
       m_run += delta;
