@@ -331,11 +331,12 @@ long long attention_d512_workspace(const AttnArgs& a) {
 }
 
 void launch_attention_d512(const AttnArgs& a, float* ws, hipStream_t s) {
-  static bool once = false;
-  if (!once) {
+  // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+  static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)&attn_d512_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS5);
-    once = true;
-  }
+    return true;
+  }();
+  (void)once;
   const int ns = ws ? d512_splits(a) : 1;
   int kps = (a.Nk + ns - 1) / ns;
   kps = (kps + KT5 - 1) / KT5 * KT5;

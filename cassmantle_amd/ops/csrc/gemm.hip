@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -51,11 +52,10 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
 bool buf_ok(const GemmArgs& p) {
-  static int force = -1;
-  if (force < 0) {
+  static const int force = [] {
     const char* e = getenv("CASSMANTLE_GEMM_BUF");
-    force = e ? atoi(e) : 1;
-  }
+    return e ? atoi(e) : 1;
+  }();
   if (p.A2 != nullptr) return true;   // two-source A exists only on this path (host-checked sizes)
   if (!force || p.K % BK != 0) return false;
   const long long ldw = p.ldw ? p.ldw : p.K;
@@ -129,9 +129,11 @@ bool deep_ok(const GemmArgs& p) {
 // ops/__init__.py): shape key -> (tile config, split-K).  Consulted before the cost model.
 std::mutex g_tune_mu;
 std::unordered_map<std::string, GemmPlan> g_tune;
-std::string g_last_key;
-GemmPlan g_last_plan{0, 1};
-bool g_record_key = false;
+// per calling thread: the generation thread and the scorer thread both launch GEMMs, and these
+// are written on every plan (tests/test_native_sanitizers.py runs the planner under TSan)
+thread_local std::string g_last_key;
+thread_local GemmPlan g_last_plan{0, 1};
+std::atomic<bool> g_record_key{false};
 
 }  // namespace
 
@@ -171,7 +173,7 @@ static int env_int(const char* name, int dflt) {
 
 // A/B knobs for the microbenchmark / tile sweeps: CASSMANTLE_GEMM_CFG=<tile index>,
 // CASSMANTLE_GEMM_SPLIT=<k slices>, or at run time gemm_set_override (tools/sweep_gemm.py)
-static int g_force_cfg = -2, g_force_split = 0;   // -2: not yet read from the environment
+static std::atomic<int> g_force_cfg{-2}, g_force_split{0};   // -2: not yet read from the environment
 void gemm_set_override(int cfg, int split) {
   g_force_cfg = cfg;
   g_force_split = split;
@@ -186,11 +188,16 @@ GemmPlan gemm_plan(const GemmArgs& p) {
 
 static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   GemmPlan best{0, 1};
-  if (g_force_cfg == -2) {
-    g_force_cfg = env_int("CASSMANTLE_GEMM_CFG", -1);
-    g_force_split = env_int("CASSMANTLE_GEMM_SPLIT", 0);
+  if (g_force_cfg.load(std::memory_order_acquire) == -2) {
+    static const bool from_env = [] {
+      g_force_split.store(env_int("CASSMANTLE_GEMM_SPLIT", 0));
+      int expect = -2;
+      g_force_cfg.compare_exchange_strong(expect, env_int("CASSMANTLE_GEMM_CFG", -1));
+      return true;
+    }();
+    (void)from_env;
   }
-  const int force_cfg = g_force_cfg, force_split = g_force_split;
+  const int force_cfg = g_force_cfg.load(), force_split = g_force_split.load();
   if (g_record_key) g_last_key = gemm_key(p);
   // in-kernel LayerNorm statistics exist only in the A-in-registers kernel (the binding checked
   // eligibility, so neither the table nor a forced config may pick anything else)

@@ -317,11 +317,12 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   const int per = (nchunks + groups - 1) / groups;
   const size_t lds = (size_t)RING * BNC * (KS / 2) * 128;
   auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU, LNK>;
-  static bool once = false;
-  if (!once) {
+  // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+  static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    once = true;
-  }
+    return true;
+  }();
+  (void)once;
   hipLaunchKernelGGL(kfn, dim3(mblocks, groups), dim3(AR_THREADS), lds, s, p, per);
 }
 
@@ -345,11 +346,10 @@ bool gemm_areg_ok(const GemmArgs& p) {
 }
 
 static int areg_variant() {
-  static int v = -2;
-  if (v == -2) {
+  static const int v = [] {
     const char* e = getenv("CASSMANTLE_AREG_V");
-    v = e ? atoi(e) : -1;
-  }
+    return e ? atoi(e) : -1;
+  }();
   return v;
 }
 

@@ -823,14 +823,13 @@ void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s
   }
 }
 
-int g_stages_override = -1;   // CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark)
-
-int stages_pref() {
-  if (g_stages_override < 0) {
+// CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark), read once
+inline int stages_pref() {
+  static const int v = [] {
     const char* e = getenv("CASSMANTLE_GEMM_STAGES");
-    g_stages_override = e ? atoi(e) : 0;
-  }
-  return g_stages_override;
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
@@ -847,11 +846,12 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
-    static bool once = false;
-    if (!once) {
+    // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+    static const bool once = [&] {
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      once = true;
-    }
+      return true;
+    }();
+    (void)once;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * WN), lds, s, p, ws);
   if (split > 1) launch_splitk_reduce<OUTF32>(p, ws, split, s);

@@ -380,11 +380,12 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   dim3 grid(nN * nM, split, p.batch);
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU>;
-  static bool once = false;
-  if (!once) {
+  // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+  static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    once = true;
-  }
+    return true;
+  }();
+  (void)once;
   hipLaunchKernelGGL(kfn, grid, dim3(512), lds, s, p, ws);
   if (split > 1) launch_splitk_reduce<false>(p, ws, split, s);
 }

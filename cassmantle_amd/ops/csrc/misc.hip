@@ -337,13 +337,14 @@ template <int C>
 void launch_blur_tile(const uint8_t* img, int H, int W, const float* w, int R, uint8_t* out, hipStream_t s) {
   const int E = BLUR_TS + 2 * R;
   const size_t lds = ((size_t)(E * E * C + 15) & ~(size_t)15) + sizeof(float) * ((size_t)E * BLUR_TS * C + 2 * R + 1);
-  static bool once = false;
-  if (!once) {    // up to ~99 KiB at R = 48 (first call happens outside any graph capture)
+  // up to ~99 KiB at R = 48 (first call happens outside any graph capture; thread-safe once)
+  static const bool once = [] {
     (void)hipFuncSetAttribute((const void*)&blur_tile_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(((size_t)(BLUR_TS + 2 * BLUR_MAXR) * (BLUR_TS + 2 * BLUR_MAXR) * C + 15 & ~(size_t)15) +
                                     sizeof(float) * ((size_t)(BLUR_TS + 2 * BLUR_MAXR) * BLUR_TS * C + 2 * BLUR_MAXR + 1)));
-    once = true;
-  }
+    return true;
+  }();
+  (void)once;
   dim3 grid((W + BLUR_TS - 1) / BLUR_TS, (H + BLUR_TS - 1) / BLUR_TS);
   hipLaunchKernelGGL(blur_tile_kernel<C>, grid, dim3(256), lds, s, img, H, W, w, R, out);
 }
