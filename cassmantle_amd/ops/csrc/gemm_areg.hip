@@ -39,9 +39,10 @@ constexpr int AR_THREADS = 256;        // 4 waves, each owning 16 * RW rows
 template <int KS, int TI, int RING>
 constexpr int areg_minb() { return RING * 16 * TI * (KS / 2) * 128 <= 80 * 1024 ? 2 : 1; }
 
-// LNK: LayerNorm folded into the GEMM with the row statistics computed here, from the A rows
-// already resident in registers (W = W * gamma, bias = bias + W . beta; epilogue
-// rstd * (acc - mean * wsum[n]) -- no LayerNorm kernel, no normalised copy, no stats pass)
+// LNK: LayerNorm applied to the A rows already resident in registers (W = W * gamma,
+// bias = bias + W . beta folded offline): row statistics from the fragments, then every
+// fragment is normalised in place to bf16 -- exactly the LayerNorm kernel's output, with no
+// LayerNorm kernel, no normalised copy in HBM, no stats pass, and a plain epilogue
 template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
 __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_areg_kernel(GemmArgs p, int chunks_per_block) {
   constexpr int AR_BM = 64 * RW;
@@ -105,6 +106,26 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
       ln_mean[j] = mu;
       ln_rstd[j] = rsqrtf(s2 * (1.f / (32 * KS)) + p.ln_eps);
     }
+    // opaque re-definition of the fragments: otherwise hipcc reuses the statistics pass's
+    // unpacked floats here and keeps all K / 4 of them live (spills)
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        i32x4_t t = __builtin_bit_cast(i32x4_t, afr[j][ks]);
+        asm volatile("" : "+v"(t));
+        afr[j][ks] = __builtin_bit_cast(bf16x8_t, t);
+      }
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float f[8];
+        unpack8(__builtin_bit_cast(uint4, afr[j][ks]), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (f[e] - ln_mean[j]) * ln_rstd[j];
+        afr[j][ks] = as_bf16x8(pack8(f));
+      }
   }
 
   // ---- W chunk staging: chunk c, LDS row (k-tile t, chunk row r) <- W row of (c, r), k 64 t..
@@ -172,7 +193,6 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
     // epilogue operands of THIS chunk, loaded BEFORE the next DMA so that waiting for them
     // (loads retire in order) leaves that DMA in flight
     uint2 bq[NQ], gq[GEGLU ? NQ : 1], rq[RW][NQ];
-    float4 wv[LNK ? NQ : 1], wg[LNK && GEGLU ? NQ : 1];   // folded-LayerNorm column sums
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int n = GEGLU ? c * (BNC / 2) + 16 * i + 4 * fq : c * BNC + 16 * i + 4 * fq;
@@ -183,10 +203,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
         bq[i] = *reinterpret_cast<const uint2*>(p.bias + n);
         if (GEGLU) gq[GEGLU ? i : 0] = *reinterpret_cast<const uint2*>(p.bias + p.N + n);
       }
-      if constexpr (LNK) {
-        wv[i] = nok ? *reinterpret_cast<const float4*>(p.ln_wsum + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (GEGLU) wg[i] = nok ? *reinterpret_cast<const float4*>(p.ln_wsum + p.N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+
 #pragma unroll
       for (int j = 0; j < RW; ++j) {
         const int m = m0 + 16 * j + fr;
@@ -242,27 +259,11 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
         if constexpr (GEGLU) {
           const uint2 g2 = gq[GEGLU ? i : 0];
           const float gb[4] = {bf2f(g2.x & 0xffff), bf2f(g2.x >> 16), bf2f(g2.y & 0xffff), bf2f(g2.y >> 16)};
-          float hv[4] = {acc[2 * i][j][0], acc[2 * i][j][1], acc[2 * i][j][2], acc[2 * i][j][3]};
-          float gv[4] = {acc[2 * i + 1][j][0], acc[2 * i + 1][j][1], acc[2 * i + 1][j][2], acc[2 * i + 1][j][3]};
-          if constexpr (LNK) {
-            const float wh[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w}, wgg[4] = {wg[i].x, wg[i].y, wg[i].z, wg[i].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              hv[e] = ln_rstd[j] * fmaf(-ln_mean[j], wh[e], hv[e]);
-              gv[e] = ln_rstd[j] * fmaf(-ln_mean[j], wgg[e], gv[e]);
-            }
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = gate_f(hv[e] + b[e], gv[e] + gb[e], p.act) + r[e];
+          for (int e = 0; e < 4; ++e) o[e] = gate_f(acc[2 * i][j][e] + b[e], acc[2 * i + 1][j][e] + gb[e], p.act) + r[e];
         } else {
-          if constexpr (LNK) {
-            const float wh[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = ln_rstd[j] * fmaf(-ln_mean[j], wh[e], acc[i][j][e]) + b[e];
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = acc[i][j][e] * p.alpha + b[e];
-          }
+          for (int e = 0; e < 4; ++e) o[e] = acc[i][j][e] * p.alpha + b[e];
           if (p.act != ACT_NONE) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = apply_act(o[e], p.act);
@@ -362,12 +363,8 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   const bool gated = is_gated(p.act);
   int v = areg_variant();
   if (v < 0) v = 2;
-  if (LNK && v == 2) v = 1;      // the 64-rows-per-wave GEGLU tile has no registers left for the stats
-  if constexpr (LNK) {
-    if (v == 2) v = 1;
-  }
   if (p.K == 320) {
-    if (!LNK && v == 2 && gated) launch_areg_t<10, 2, 3, 4, true, false>(p, s);   // RW = 4 spills without the gate pairing
+    if (v == 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
     else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
     else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
   } else {
