@@ -75,6 +75,11 @@ class GameConfig:
     rank_stale_s: float = 30.0            # a heartbeat older than this marks the rank dead
     round_timeout_s: float = 600.0        # a generation round running longer degrades to local
     exit_on_rank_failure: bool = False    # after degrading: snapshot + exit 3 for a supervisor
+    # --- multi-GPU guess scoring (parallel/scoring.py) ---
+    score_topology: str = "central"       # central (rank 0 scores) | sharded (C1 broadcast + C3 gather)
+    score_shard_min: int = 256            # sharded: smaller micro-batches are still scored on rank 0
+    score_timeout_s: float = 30.0         # sharded: a slower scoring round degrades to rank-0-local
+    score_group_backend: str = "gloo"     # sharded: transport of the scoring group (gloo | nccl)
 
 
 @dataclass

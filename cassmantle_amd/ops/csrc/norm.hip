@@ -16,6 +16,8 @@
 // LayerNorm: T = 2..64 lanes per row (T*8*VPL >= D), 64/T rows per wave, row held in
 // registers, two-pass mean/variance, xor-shuffle reductions inside the T-lane segment
 // (v0 used one wave per row: 40 of 64 lanes busy at D = 320).
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -489,10 +491,10 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        chunks, rpc);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(G, B), dim3(64), 0, s, part, stats, S, C, G, chunks, eps);
   // apply: ~8 rows per row-lane per block
-  long long rpb = 8LL * g.R;
+  long long rpb = 2LL * GN_UNROLL * g.R;                   // whole GN_UNROLL-row iterations per thread
   long long nb = (S + rpb - 1) / rpb;
-  if (nb * B < 1024) {                                     // small images: shorter blocks, more of them
-    rpb = (long long)g.R * 2;
+  if (nb * B < 2048) {                                     // small images: shorter blocks, more of them
+    rpb = (long long)GN_UNROLL * g.R;
     nb = (S + rpb - 1) / rpb;
   }
   if (g.VPT == 1)
@@ -507,12 +509,31 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long
                           const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
                           int G, float eps, int silu, hipStream_t s) {
   const GnGeom g = gn_geom(C);
-  long long rpb = 8LL * g.R;
-  long long nb = (S + rpb - 1) / rpb;
-  if (nb * B < 1024) {
-    rpb = (long long)g.R * 2;
+  // every thread runs whole GN_UNROLL-row iterations (GN_UNROLL independent 16-byte loads in
+  // flight): the old fallback to 2 rows per thread for short grids left one dependent load per
+  // thread at a time and ran the SD-1.5 level-1 apply at ~3.2 TB/s
+  // ... and blocks long enough to amortise the prologue (every block first reads all C channel
+  // statistics, 16 B each: at C = 1280 a 4-row block reads twice its own data): at least 32 rows
+  // and 32 KiB of activations per block, shortened only while that leaves fewer than ~1024 blocks
+  // (the 16^2 / 8^2 levels), and down to half an iteration when even one iteration per thread
+  // leaves fewer than 256 blocks (8^2 x 2560: 2 rows per thread on 256 blocks beats 4 on 128).
+  // profiles/r2_gn_rows_ab.txt has the per-shape A/B; CASSMANTLE_GN_ROWS=-1 restores the
+  // round-1 rule (A/B knob)
+  static const int mode = [] { const char* e = getenv("CASSMANTLE_GN_ROWS"); return e ? atoi(e) : 0; }();
+  const long long step = (long long)GN_UNROLL * g.R;
+  long long rpb, nb;
+  if (mode < 0) {
+    rpb = 8LL * g.R;
     nb = (S + rpb - 1) / rpb;
+    if (nb * B < 1024) rpb = 2LL * g.R;
+  } else {
+    long long want = 32;
+    if (want < (32LL << 10) / (2LL * C)) want = (32LL << 10) / (2LL * C);
+    rpb = step * ((want + step - 1) / step);
+    while (rpb > step && ((S + rpb - 1) / rpb) * B < 1024) rpb -= step;
+    if (rpb == step && ((S + rpb - 1) / rpb) * B < 256) rpb = step / 2 >= g.R ? step / 2 : g.R;
   }
+  nb = (S + rpb - 1) / rpb;
   const size_t shs = sizeof(float) * 2 * G + sizeof(long long) * 2 * C;
   if (stats_b == nullptr) Ca = C;
   if (g.VPT == 1)

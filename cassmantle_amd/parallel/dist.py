@@ -63,11 +63,11 @@ def shutdown() -> None:
         dist.destroy_process_group()
 
 
-def broadcast_object(obj: Any, src: int = 0) -> Any:
+def broadcast_object(obj: Any, src: int = 0, group=None) -> Any:
     if not (dist.is_available() and dist.is_initialized()):
         return obj
     lst = [obj]
-    dist.broadcast_object_list(lst, src=src)
+    dist.broadcast_object_list(lst, src=src, group=group)
     return lst[0]
 
 

@@ -32,7 +32,9 @@ def model_dtype(cfg: Config, device: str) -> torch.dtype:
     return dt
 
 
-def build_scorer(cfg: Config, device: Optional[str] = None):
+def build_scorer(cfg: Config, device: Optional[str] = None, wrap=None):
+    """MiniLM-encoder (or word-vector) backend behind the micro-batching scorer.  ``wrap`` maps
+    the local backend to the one the scorer calls (multi-GPU: ``parallel.scoring.ShardedSimilarity``)."""
     dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
     if cfg.model.scorer == "wordvec":
         from ..scoring.wordvec import WordVectorBackend
@@ -47,6 +49,8 @@ def build_scorer(cfg: Config, device: Optional[str] = None):
             missing = load_bert(backend.model, read_safetensors(cfg.model.scorer_weights))
             if missing:
                 raise KeyError(f"scorer_weights: {len(missing)} tensors missing, e.g. {missing[:3]}")
+    if wrap is not None:
+        backend = wrap(backend)
     return BatchingScorer(backend, cfg.game.min_score, window_ms=cfg.model.scorer_batch_window_ms)
 
 
@@ -111,8 +115,8 @@ def build_image_generator(cfg: Config, device: Optional[str] = None) -> ImageGen
 
 
 def build_service(cfg: Config, image_gen_for_room: Optional[Callable[[str], ImageGenerator]] = None,
-                  **kw) -> GameService:
-    scorer = build_scorer(cfg)
+                  scorer=None, **kw) -> GameService:
+    scorer = scorer if scorer is not None else build_scorer(cfg)
     if image_gen_for_room is None:
         # one device pipeline shared by every room: requests are serialised and batched
         gen = BatchingImageGenerator(build_image_generator(cfg), max_batch=cfg.model.gen_batch_max,

@@ -57,12 +57,31 @@ def main(argv=None) -> int:
     store = tdist.distributed_c10d._get_default_store()
     hb = HeartbeatMonitor(store, ctx.rank, ctx.world_size, period_s=cfg.game.rank_heartbeat_s,
                           stale_s=cfg.game.rank_stale_s).start()
+    g = cfg.game
+    if g.score_topology not in ("central", "sharded"):
+        raise ValueError(f"score_topology must be central or sharded, got {g.score_topology!r}")
+    sharded = None
+    holder = {}
+    if g.score_topology == "sharded":                  # C1 + C3 on a scoring group of its own
+        from .parallel.scoring import ShardedSimilarity, new_scoring_group
+        from .runtime.factory import build_scorer
+        sgroup = new_scoring_group(g.score_group_backend)
+
+        def wrap(local):
+            nonlocal sharded
+            sharded = ShardedSimilarity(ctx, local, group=sgroup, min_pairs=g.score_shard_min,
+                                        timeout_s=g.score_timeout_s,
+                                        healthy=lambda: holder.get("coord") is None or holder["coord"].degraded is None)
+            return sharded
+        scorer = build_scorer(cfg, device=str(ctx.device), wrap=wrap)
     if ctx.rank != 0:
+        st = sharded.start_serving() if sharded is not None else None
         worker.serve_forever()
+        if st is not None:
+            st.join(timeout=g.score_timeout_s)
         hb.stop()
         cdist.shutdown()
         return 0
-    holder = {}
 
     def on_degraded(reason: str) -> None:
         # rooms keep serving from rank 0's GPU; optionally hand over to a supervisor restart
@@ -75,12 +94,16 @@ def main(argv=None) -> int:
 
     coord = GenerationCoordinator(worker, monitor=hb, round_timeout_s=cfg.game.round_timeout_s,
                                   on_degraded=on_degraded)
-    svc = build_service(cfg, image_gen_for_room=lambda rid: RankImageGenerator(coord, rid), room_ids=room_ids)
+    holder["coord"] = coord
+    svc = build_service(cfg, image_gen_for_room=lambda rid: RankImageGenerator(coord, rid), room_ids=room_ids,
+                        scorer=scorer if sharded is not None else None)
     holder["svc"] = svc
     app = create_app(svc, cfg)
     try:
         uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
     finally:
+        if sharded is not None:
+            sharded.close()
         coord.close()
         hb.stop()
         if coord.degraded is None:

@@ -1,8 +1,10 @@
 """BASELINE config 5: a live round — image generation and streaming guess scoring overlapped.
 
 The SERVING topology (``serve.py``): every rank (one per GPU, ``torchrun`` for N > 1) generates
-its rooms' content; ALL guess scoring runs on rank 0, next to the front-end that owns every
-session (a guess costs microseconds of GPU time, so a cross-rank hop would only add latency):
+its rooms' content; guess scoring runs on rank 0, next to the front-end that owns every session
+(a guess costs microseconds of GPU time, so a cross-rank hop would only add latency), unless
+``--score-topology sharded`` (serve.py's ``score_topology=sharded``) splits large micro-batches
+over every rank with a C1 broadcast + C3 score gather (``parallel/scoring.py``):
 
 * on every rank a generation thread replays the hipGraph-captured SD-1.5 denoise loop back to
   back (batch 4 images per room, 512², 50 PNDM steps) on the pipeline's own stream;
@@ -48,6 +50,10 @@ def parse():
                          "on the legacy default stream it queued behind whole generations, "
                          "pipeline.StableDiffusion.generate_tensor docstring)")
     ap.add_argument("--window-ms", type=float, default=1.0)
+    ap.add_argument("--score-topology", choices=("central", "sharded"), default="central",
+                    help="as serve.py's GameConfig.score_topology: rank-0 scoring, or micro-batches of "
+                         ">= --shard-min pairs split over every rank (C1 broadcast + C3 gather, parallel/scoring.py)")
+    ap.add_argument("--shard-min", type=int, default=256)
     return ap.parse_args()
 
 
@@ -85,6 +91,13 @@ def main():
     n_players = a.players if rank == 0 else 0          # rank-0-central scoring, as serve.py
     sd = StableDiffusion(SPECS[a.model], device=dev, seed=0)
     backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
+    sharded = follower = None
+    if a.score_topology == "sharded" and world > 1:
+        from cassmantle_amd.parallel.scoring import ShardedSimilarity, new_scoring_group
+        sharded = ShardedSimilarity(ctx, backend, group=new_scoring_group("gloo"), min_pairs=a.shard_min)
+        backend = sharded
+        if rank != 0:
+            follower = sharded.start_serving()
     scorer = BatchingScorer(backend, 0.01, window_ms=a.window_ms)
     gen = SyntheticPromptGenerator(salt=rank)
     seeds_txt, styles = load_seeds(), load_styles()
@@ -131,6 +144,10 @@ def main():
     elapsed = time.perf_counter() - t0
     stop.set()
     th.join()
+    if sharded is not None:
+        sharded.close()                                # rank 0: STOP to the followers
+        if follower is not None:
+            follower.join(timeout=60)
 
     def pct(x, q):
         return float(np.percentile(np.asarray(x), q)) if x else float("nan")
@@ -151,6 +168,8 @@ def main():
             "think_ms": a.think_ms, "idle_p50_ms": round(s[1], 3), "idle_p99_ms": round(s[2], 3),
             "load_p50_ms": round(s[3], 3), "load_p99_ms": round(s[4], 3), "requests": int(s[5]),
             "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
+            "score_topology": a.score_topology,
+            "sharded_pairs": sharded.sharded_pairs if sharded is not None else 0,
             "config": {"model": a.model, "batch_per_room": a.batch, "graphs": bool(sd.use_graphs)}}), flush=True)
     cdist.shutdown()
 
