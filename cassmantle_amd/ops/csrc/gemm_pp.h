@@ -60,8 +60,13 @@ constexpr size_t pp_lds_bytes() {
   return st > ep ? st : ep;
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU>
+// SCHED: 0 = four quadrant phases per k-tile (J0 loads W-a and A-a), 1 = four phases with the
+// W-a load moved to J3 of the previous k-tile, 2 = two phases per k-tile (W-a x A, W-b x A).
+// DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
+// DMA, bit 1 its barriers
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __restrict__ partial) {
+  constexpr bool SPREAD = SCHED == 1;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   using G = PPGeom<BM, BN, WM, WN>;
   static_assert(WM * WN == 8, "8 waves");
@@ -268,7 +273,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8_t wf[TIa > TIb ? TIa : TIb][2];   // W fragments of the current n-half
+  bf16x8_t wfa[TIa][2], wfb[TIb][2];      // W fragments of both n-halves
   bf16x8_t afa[TJa][2], afb[TJb][2];       // A fragments of both m-halves
 
   // ---- prologue: parts 0..5 (k-tile 0 whole, k-tile 1 A-a / W-a), then retire k-tile 0's
@@ -280,17 +285,37 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
     stage(I3{}, kt0, 0);
   }
   if (nk > 1) {
-    stage(I0{}, kt0 + 1, 1);
-    stage(I1{}, kt0 + 1, 1);
-    wait_vmcnt<G::PERIOD>();
+    if constexpr (SCHED == 2) {            // k-tile 1's A halves (issued by "P1 of k-tile -1")
+      stage(I0{}, kt0 + 1, 1);
+      stage(I2{}, kt0 + 1, 1);
+      wait_vmcnt<G::NR0 + G::NR2>();
+    } else if constexpr (SPREAD) {
+      stage(I1{}, kt0 + 1, 1);
+      stage(I0{}, kt0 + 1, 1);
+      wait_vmcnt<G::PERIOD>();
+    } else {
+      stage(I0{}, kt0 + 1, 1);
+      stage(I1{}, kt0 + 1, 1);
+      wait_vmcnt<G::PERIOD>();
+    }
   } else {
     wait_vmcnt<0>();
   }
   __builtin_amdgcn_s_barrier();
   if (late) __builtin_amdgcn_s_barrier();
+  if constexpr (SPREAD) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TIa; ++i) wfa[i][ks] = as_bf16x8(smem[wbase_a + 128 * i + lo[ks]]);
+  }
 
-  // one phase: quadrant J of local k-tile t (buffer B); issues the part scheduled 5-6 phases
-  // ahead; waits so that every part issued >= 4 phases ago has landed (reads of phase q+1)
+  // one phase: quadrant J of local k-tile t (buffer B).  Fragment reads are spread so no phase
+  // carries more than one operand half: J0 A-a, J1 A-b, J2 W-b, J3 W-a of the NEXT k-tile (from
+  // the other buffer; the quadrant order (a,a) (a,b) (b,b) (b,a) leaves W-a idle in J2/J3), which
+  // is why W-a of tile t+2 is staged in J2 and A-a in J3.  Issues the part scheduled 5-6 phases
+  // ahead of its first read and >= 3 phases after the last read of the bytes it overwrites;
+  // waits so that every part issued >= 4 phases ago has landed (reads of phase q+1)
   auto phase = [&](auto Jc, auto Bc, int t) {
     constexpr int J = decltype(Jc)::value;
     constexpr int B = decltype(Bc)::value;
@@ -298,8 +323,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
     if constexpr (J == 0) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (!SPREAD) {
 #pragma unroll
-        for (int i = 0; i < TIa; ++i) wf[i][ks] = as_bf16x8(Bs[wbase_a + 128 * i + lo[ks]]);
+          for (int i = 0; i < TIa; ++i) wfa[i][ks] = as_bf16x8(Bs[wbase_a + 128 * i + lo[ks]]);
+        }
 #pragma unroll
         for (int j = 0; j < TJa; ++j) afa[j][ks] = as_bf16x8(Bs[abase_a + 128 * j + lo[ks]]);
       }
@@ -312,57 +339,159 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < TIb; ++i) wf[i][ks] = as_bf16x8(Bs[wbase_b + 128 * i + lo[ks]]);
+        for (int i = 0; i < TIb; ++i) wfb[i][ks] = as_bf16x8(Bs[wbase_b + 128 * i + lo[ks]]);
+    } else if constexpr (SPREAD) {           // W-a of the next k-tile (other buffer; garbage past nk)
+      const uint4* Bn = smem + (B ^ 1) * TILE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TIa; ++i) wfa[i][ks] = as_bf16x8(Bn[wbase_a + 128 * i + lo[ks]]);
     }
-    // part issued now: J=0 -> A-b of tile t+1, J=1 -> W-b of t+1, J=2 -> A-a of t+2, J=3 -> W-a of t+2
+    // part issued now: J=0 -> A-b of tile t+1, J=1 -> W-b of t+1, J=2 -> W-a of t+2, J=3 -> A-a of t+2
     constexpr int DU = (J + 2) >> 2 ? 2 : 1;
     const int u = t + DU;                  // local tile index of the part
-    const bool issue = u < nk;
+    const bool issue = !(DIAG & 1) && u < nk;
     if (issue) {
       if constexpr (J == 0) stage(I2{}, kt0 + u, B ^ 1);
       else if constexpr (J == 1) stage(I3{}, kt0 + u, B ^ 1);
-      else if constexpr (J == 2) stage(I0{}, kt0 + u, B);
-      else stage(I1{}, kt0 + u, B);
+      else if constexpr (J == 2) { if constexpr (SPREAD) stage(I1{}, kt0 + u, B); else stage(I0{}, kt0 + u, B); }
+      else { if constexpr (SPREAD) stage(I0{}, kt0 + u, B); else stage(I1{}, kt0 + u, B); }
       wait_vmcnt<G::PERIOD>();
     } else {
       wait_vmcnt<0>();
     }
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
     wait_lgkm<0>();
     __builtin_amdgcn_s_setprio(1);
-    constexpr int I_LO = (J == 0 || J == 1) ? 0 : TIa;
-    constexpr int I_N = (J == 0 || J == 1) ? TIa : TIb;
-    constexpr bool MA = (J == 0 || J == 3);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks) {
+      if constexpr (J == 0 || J == 1) {
 #pragma unroll
-      for (int i = 0; i < I_N; ++i) {
-        if constexpr (MA) {
+        for (int i = 0; i < TIa; ++i) {
+          if constexpr (J == 0) {
 #pragma unroll
-          for (int j = 0; j < TJa; ++j)
-            acc[I_LO + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][ks], afa[j][ks], acc[I_LO + i][j], 0, 0, 0);
-        } else {
+            for (int j = 0; j < TJa; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfa[i][ks], afa[j][ks], acc[i][j], 0, 0, 0);
+          } else {
 #pragma unroll
-          for (int j = 0; j < TJb; ++j)
-            acc[I_LO + i][TJa + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][ks], afb[j][ks], acc[I_LO + i][TJa + j], 0, 0, 0);
+            for (int j = 0; j < TJb; ++j)
+              acc[i][TJa + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfa[i][ks], afb[j][ks], acc[i][TJa + j], 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TIb; ++i) {
+          if constexpr (J == 3) {
+#pragma unroll
+            for (int j = 0; j < TJa; ++j)
+              acc[TIa + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[i][ks], afa[j][ks], acc[TIa + i][j], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int j = 0; j < TJb; ++j)
+              acc[TIa + i][TJa + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[i][ks], afb[j][ks], acc[TIa + i][TJa + j], 0, 0, 0);
+          }
         }
       }
+    }
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
+  };
+
+  // SCHED 2: two phases per k-tile t (buffer B), each one MFMA cluster twice as long as a
+  // quadrant's.  P0 reads W-a, A-a, A-b of t and issues W-a, W-b of t+1 (other buffer, whose W
+  // regions were last read in P0 / P1 of t-1); P1 reads W-b of t and issues A-a, A-b of t+2 (this
+  // buffer, A regions last read in P0 of t).  Every phase waits for all parts but its own, so the
+  // parts the next phase reads have landed before the barrier that publishes them; the reads wait
+  // for their data BEFORE the barrier because the other half overwrites bytes read in phase q
+  // right after the barrier of phase q+1.
+  auto mphase = [&](auto Pc, auto Bc, int t) {
+    constexpr int P = decltype(Pc)::value;
+    constexpr int B = decltype(Bc)::value;
+    const uint4* Bs = smem + B * TILE;
+    if constexpr (P == 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < TIa; ++i) wfa[i][ks] = as_bf16x8(Bs[wbase_a + 128 * i + lo[ks]]);
+#pragma unroll
+        for (int j = 0; j < TJa; ++j) afa[j][ks] = as_bf16x8(Bs[abase_a + 128 * j + lo[ks]]);
+#pragma unroll
+        for (int j = 0; j < TJb; ++j) afb[j][ks] = as_bf16x8(Bs[abase_b + 128 * j + lo[ks]]);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TIb; ++i) wfb[i][ks] = as_bf16x8(Bs[wbase_b + 128 * i + lo[ks]]);
+    }
+    const int u = t + (P == 0 ? 1 : 2);
+    if (!(DIAG & 1) && u < nk) {
+      if constexpr (P == 0) {
+        stage(I1{}, kt0 + u, B ^ 1);
+        stage(I3{}, kt0 + u, B ^ 1);
+        wait_vmcnt<G::NR1 + G::NR3>();
+      } else {
+        stage(I0{}, kt0 + u, B);
+        stage(I2{}, kt0 + u, B);
+        wait_vmcnt<G::NR0 + G::NR2>();
+      }
+    } else {
+      wait_vmcnt<0>();
+    }
+    wait_lgkm<0>();
+    if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if constexpr (P == 0) {
+#pragma unroll
+        for (int i = 0; i < TIa; ++i) {
+#pragma unroll
+          for (int j = 0; j < TJa; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfa[i][ks], afa[j][ks], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < TJb; ++j)
+            acc[i][TJa + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfa[i][ks], afb[j][ks], acc[i][TJa + j], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TIb; ++i) {
+#pragma unroll
+          for (int j = 0; j < TJb; ++j)
+            acc[TIa + i][TJa + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[i][ks], afb[j][ks], acc[TIa + i][TJa + j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < TJa; ++j)
+            acc[TIa + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[i][ks], afa[j][ks], acc[TIa + i][j], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
   };
 
   // two k-tiles per iteration so the buffer of every phase is a compile-time offset
-  for (int t = 0; t < nk; t += 2) {
-    phase(I0{}, I0{}, t);
-    phase(I1{}, I0{}, t);
-    phase(I2{}, I0{}, t);
-    phase(I3{}, I0{}, t);
-    if (t + 1 >= nk) break;
-    phase(I0{}, I1{}, t + 1);
-    phase(I1{}, I1{}, t + 1);
-    phase(I2{}, I1{}, t + 1);
-    phase(I3{}, I1{}, t + 1);
+  if constexpr (SCHED == 2) {
+    for (int t = 0; t < nk; t += 2) {
+      mphase(I0{}, I0{}, t);
+      mphase(I1{}, I0{}, t);
+      if (t + 1 >= nk) break;
+      mphase(I0{}, I1{}, t + 1);
+      mphase(I1{}, I1{}, t + 1);
+    }
+  } else {
+    for (int t = 0; t < nk; t += 2) {
+      phase(I0{}, I0{}, t);
+      phase(I1{}, I0{}, t);
+      phase(I2{}, I0{}, t);
+      phase(I3{}, I0{}, t);
+      if (t + 1 >= nk) break;
+      phase(I0{}, I1{}, t + 1);
+      phase(I1{}, I1{}, t + 1);
+      phase(I2{}, I1{}, t + 1);
+      phase(I3{}, I1{}, t + 1);
+    }
   }
   if (!late) __builtin_amdgcn_s_barrier();   // re-align the two halves
   wait_vmcnt<0>();
@@ -379,7 +508,11 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   const int split = (ws != nullptr && p.split > 1) ? p.split : 1;
   dim3 grid(nN * nM, split, p.batch);
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
-  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU>;
+  // CASSMANTLE_PP_SCHED=0|1|2 picks the mainloop schedule (gemm_pp_kernel SCHED), A/B knob
+  static const int sched = [] { const char* e = getenv("CASSMANTLE_PP_SCHED"); return e ? atoi(e) : 2; }();
+  auto* kfn = sched == 2   ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>
+              : sched == 1 ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 1>
+                           : &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 0>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
