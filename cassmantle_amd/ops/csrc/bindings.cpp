@@ -109,7 +109,9 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     TORCH_CHECK(p.M > 8 && p.K % 8 == 0 && p.lda % 8 == 0 && !p.out_f32, "gemm: folded LayerNorm needs the MFMA path");
     p.ln_wsum = ln_wsum->data_ptr<float>();
     p.ln_eps = (float)ln_eps;
-    if (!gemm_areg_ok(p)) {
+    // CASSMANTLE_LN_INKERNEL=0 forces the row-statistics pass (A/B and debugging knob)
+    static const bool inkernel = [] { const char* e = getenv("CASSMANTLE_LN_INKERNEL"); return !(e && e[0] == '0'); }();
+    if (!inkernel || !gemm_areg_ok(p)) {
       TORCH_CHECK(x.is_contiguous() && p.K <= 4096, "gemm: folded LayerNorm row statistics need contiguous rows");
       at::Tensor rows = at::empty({p.M, 2}, x.options().dtype(at::kFloat));
       launch_row_stats(bptr(x), rows.data_ptr<float>(), p.M, p.K, (float)ln_eps, cur_stream());

@@ -302,6 +302,10 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
       }
     }
   }
+  // the ring always has a chunk's DMA in flight (the zero-filled stage past the block's range
+  // included): drain it before the workgroup retires, or it lands in the LDS of the next
+  // workgroup placed on this CU (a run-to-run race: tools/dbg_det_ops.py)
+  areg_wait_vmcnt<0>();
 }
 
 template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
@@ -316,6 +320,7 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   const int target = 256 * areg_minb<KS, TI, RING>();
   while (mblocks * groups < target && nchunks / (groups * 2) >= 2) groups *= 2;
   const int per = (nchunks + groups - 1) / groups;
+  groups = (nchunks + per - 1) / per;   // no block without chunks
   const size_t lds = (size_t)RING * BNC * (KS / 2) * 128;
   auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU, LNK>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
@@ -368,8 +373,10 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
     else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
     else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
   } else {
+    // (the 16-row-chunk variant with the in-kernel LayerNorm gives run-to-run different results
+    // at the last bit -- tools/dbg_det_lnk.py; cause not found -- so LNK takes the 32-row chunks)
     if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
-    else if (v >= 1) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
+    else if (v >= 1 && !LNK) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
     else launch_areg_t<20, 2, 3, 2, false, LNK>(p, s);
   }
 }

@@ -62,6 +62,8 @@ constexpr size_t pp_lds_bytes() {
 
 // SCHED: 0 = four quadrant phases per k-tile (J0 loads W-a and A-a), 1 = four phases with the
 // W-a load moved to J3 of the previous k-tile, 2 = two phases per k-tile (W-a x A, W-b x A).
+// (Reading the next phase's fragments inside the current MFMA cluster was tried: slower on every
+// tile, and the early half would read parts the late half has not waited for; profiles/r2_ppdiag_sched3.jsonl.)
 // DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
 // DMA, bit 1 its barriers
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0>
@@ -285,7 +287,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
     stage(I3{}, kt0, 0);
   }
   if (nk > 1) {
-    if constexpr (SCHED == 2) {            // k-tile 1's A halves (issued by "P1 of k-tile -1")
+    if constexpr (SCHED >= 2) {            // k-tile 1's A halves (issued by "P1 of k-tile -1")
       stage(I0{}, kt0 + 1, 1);
       stage(I2{}, kt0 + 1, 1);
       wait_vmcnt<G::NR0 + G::NR2>();
@@ -510,7 +512,7 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   // CASSMANTLE_PP_SCHED=0|1|2 picks the mainloop schedule (gemm_pp_kernel SCHED), A/B knob
   static const int sched = [] { const char* e = getenv("CASSMANTLE_PP_SCHED"); return e ? atoi(e) : 2; }();
-  auto* kfn = sched == 2   ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>
+  auto* kfn = sched >= 2 ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>
               : sched == 1 ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 1>
                            : &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 0>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)

@@ -44,7 +44,9 @@ def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> Di
         device = torch.device("cpu")
     be = None
     if world > 1:
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # CASSMANTLE_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on ONE GPU
+        # (RCCL refuses two ranks on a device); production is always nccl (= RCCL) on GPUs
+        be = backend or os.environ.get("CASSMANTLE_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":

@@ -105,9 +105,9 @@ int main() {
     p.M = B * H * H; p.K = 9 * C; p.lda = C; p.ldc = C; p.stride = 1; p.pad = 1;
     const double fl = 2.0 * p.M * p.N * p.K;
     for (int rep = 0; rep < 2; ++rep) {
-      arms<256, 160, 4, 2, 2, 0>("conv64_320", p, fl, 20);
-      arms<256, 160, 4, 2, 2, 1>("conv64_320", p, fl, 20);
       arms<256, 160, 4, 2, 2, 2>("conv64_320", p, fl, 20);
+      arms<256, 128, 4, 2, 2, 2>("conv64_320", p, fl, 20);
+      arms<256, 256, 4, 2, 2, 2>("conv64_320", p, fl, 20);
     }
   }
   {
@@ -121,9 +121,9 @@ int main() {
     p.M = M; p.N = N; p.Nw = N; p.K = K; p.lda = K; p.ldc = N;
     const double fl = 2.0 * M * N * K;
     for (int rep = 0; rep < 2; ++rep) {
-      arms<256, 256, 4, 2, 0, 0>("gemm4096", p, fl, 10);
-      arms<256, 256, 4, 2, 0, 1>("gemm4096", p, fl, 10);
       arms<256, 256, 4, 2, 0, 2>("gemm4096", p, fl, 10);
+      arms<256, 160, 4, 2, 0, 2>("gemm4096", p, fl, 10);
+      arms<128, 256, 2, 4, 0, 2>("gemm4096", p, fl, 10);
     }
   }
   CK(hipDeviceSynchronize());
