@@ -67,13 +67,17 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     # fragments; past the default limit the unroller gives up and the accumulators go to scratch
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result", "-Wno-unused-variable",
               "-mllvm", "-pragma-unroll-threshold=100000"]
+    # per-file extra flags.  gemm_areg: no SLP vectorisation (no packed-fp32 v_pk_* VALU in the
+    # in-kernel LayerNorm and the epilogues; see the LNK block of gemm_areg.hip)
+    file_flags = {"gemm_areg.hip": ["-fno-slp-vectorize"]}
     cmds = []
     objs = []
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(src, obj, headers):
-            cmds.append([hipcc, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", src, "-o", obj])
+            cmds.append([hipcc, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common,
+                         *file_flags.get(os.path.basename(src), []), "-c", src, "-o", obj])
     bobj = os.path.join(BUILD, "bindings.o")
     objs.append(bobj)
     if force or _newer(binding, bobj, headers):

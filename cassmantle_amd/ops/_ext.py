@@ -19,6 +19,10 @@ _tried = False
 
 
 def so_path() -> Optional[str]:
+    # CASSMANTLE_EXT_SO: load another build of the extension (same-box A/B of compile options)
+    alt = os.environ.get("CASSMANTLE_EXT_SO") or None
+    if alt:
+        return alt
     cands = sorted(glob.glob(os.path.join(_PKG, "_C*.so")))
     return cands[0] if cands else None
 

@@ -29,6 +29,18 @@ CM_DEVICE void areg_blds16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, int 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, voff, soff, 0, 0);
 }
 
+// sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (the 4 lanes holding one A row) with the gfx950
+// permlane swaps: pure VALU, no ds_bpermute through the LDS unit.  The in-kernel LayerNorm
+// statistics went wrong under two-stream concurrency with __shfl_xor (see the LNK block)
+CM_DEVICE float sum_row_groups(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // rows (0,0,2,2) | (1,1,3,3)
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const unsigned w = __float_as_uint(s);
+  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);   // halves (lo,lo) | (hi,hi)
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 template <int N>
 CM_DEVICE void areg_wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -97,10 +109,8 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
           s2 = fmaf(lo, lo, fmaf(hi, hi, s2));
         }
       }
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
+      s1 = sum_row_groups(s1);
+      s2 = sum_row_groups(s2);
       const float mu = s1 * (1.f / (32 * KS));
       s2 = fmaxf(s2 * (1.f / (32 * KS)) - mu * mu, 0.f) * (32 * KS);
       ln_mean[j] = mu;
@@ -125,6 +135,23 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = (f[e] - ln_mean[j]) * ln_rstd[j];
         afr[j][ks] = as_bf16x8(pack8(f));
+      }
+    // Finish the statistics before the first W-chunk LDS-DMA.  Their cross-lane sums are
+    // ds_bpermute (__shfl_xor) reads through the LDS unit, and the scheduler used to place them
+    // after the first LDS-DMAs.  While those DMAs were in flight, the shuffles' partial lgkmcnt
+    // waits did not cover them.  Whole 16-row groups then came out with a wrong mean/rstd (up to
+    // 0.1 abs), but only when another kernel slowed the DMA down: a 4-wave GEMM on a second
+    // stream, or stage-overlapped VAE decode (tools/dbg_conc_matrix.py, tools/dbg_overlap.py).
+    // The opaque asm below makes the normalised fragments inputs of a memory-clobbering
+    // statement, so no DMA can be scheduled above the statistics.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        i32x4_t t = __builtin_bit_cast(i32x4_t, afr[j][ks]);
+        asm volatile("" : "+v"(t) : : "memory");
+        afr[j][ks] = __builtin_bit_cast(bf16x8_t, t);
       }
   }
 

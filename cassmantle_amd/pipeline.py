@@ -270,6 +270,7 @@ class StableDiffusion:
                 x = self.denoise(ctx, x0, plan, added)
             self.last_finite = torch.isfinite(x).all()
             z = x.to(self.dtype)
+            self.last_latents = z
             if self.decode_stream is None:
                 with span("decode", self.stream):
                     img = self.vae.decode_uint8(z)
