@@ -203,9 +203,12 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
   };
 
   const int hw = p.stats_hw > 0 ? p.stats_hw : 1;
-  static_assert(RING == 3, "one chunk in flight behind the one being retired");
+  // RING 3: one chunk in flight behind the one being retired.  RING 2 (plain double buffer):
+  // the next chunk's DMA overlaps this chunk's MFMAs and epilogue and is retired at the top of
+  // the next iteration; 2/3 of the LDS, so the K = 640 tiles fit 2 blocks per CU
+  static_assert(RING == 2 || RING == 3, "2- or 3-deep ring");
   stage(c_begin, 0);
-  stage(c_begin + 1, 1);
+  if constexpr (RING == 3) stage(c_begin + 1, 1);
 
   constexpr int NQ = GEGLU ? TI / 2 : TI;          // output column quads per row per chunk
   for (int c = c_begin; c < c_end; ++c) {
@@ -213,7 +216,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
     const int buf = rel % RING;
     // retire chunk c (chunk c + 1 stays in flight), publish it.  After the first chunk this is
     // already satisfied by the previous chunk's epilogue wait.
-    areg_wait_vmcnt<DMA_PER_CHUNK>();
+    areg_wait_vmcnt<(RING - 2) * DMA_PER_CHUNK>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();            // chunk c landed; every wave is done with c-1's buffer
 
@@ -389,20 +392,23 @@ static int areg_variant() {
 // Instantiations (measured on the SD-1.5 batch-8 level-1/2 shapes, profiles/r2_areg_variants.jsonl):
 //   v0: 40 KiB chunks, 1 block / CU               v1: 20 KiB chunks, 2 blocks / CU
 //   v2: v1 with 64 rows per wave for gated K = 320 (each LDS W fragment feeds 4 MFMAs, not 2)
-// default (-1): v2 for the K = 320 GEGLU (127 -> 70 us), v1 otherwise
+//   v3: v2, and the K = 640 tiles on a 2-deep ring (80 KiB: 2 blocks per CU instead of 1)
+// default (-1): v3 (K = 640 ring 2: 585 -> 580 ms/step same box x3, profiles/r2_areg_ring2_ab.txt)
 template <bool LNK>
 void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   const bool gated = is_gated(p.act);
   int v = areg_variant();
-  if (v < 0) v = 2;
+  if (v < 0) v = 3;
   if (p.K == 320) {
-    if (v == 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
+    if (v >= 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
     else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
     else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
   } else {
     // (the 16-row-chunk variant with the in-kernel LayerNorm gives run-to-run different results
     // at the last bit -- tools/dbg_det_lnk.py; cause not found -- so LNK takes the 32-row chunks)
-    if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
+    // v3: 2-deep ring (80 KiB, 2 blocks per CU) for the 32-row chunks
+    if (v == 3) gated ? launch_areg_t<20, 2, 2, 2, true, LNK>(p, s) : launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
+    else if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
     else if (v >= 1 && !LNK) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
     else launch_areg_t<20, 2, 3, 2, false, LNK>(p, s);
   }
