@@ -63,7 +63,8 @@ def load_gemm_tuning(path: Optional[str] = None) -> int:
     if _tune_loaded and path is None:
         return ext().gemm_tune_size()
     import json
-    p = path or _TUNE_PATH
+    # CASSMANTLE_GEMM_TUNE_PATH: another table (same-box A/B of two tables)
+    p = path or os.environ.get("CASSMANTLE_GEMM_TUNE_PATH") or _TUNE_PATH
     _tune_loaded = True
     if not os.path.exists(p):
         return 0

@@ -222,35 +222,42 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
                                                                  uint16_t* __restrict__ y, long long S, int C,
                                                                  int G, int T, int R, long long rows_per_block,
                                                                  float eps, int silu) {
-  extern __shared__ float gst[];           // [G][2] mean, rstd, then [C][2] channel sums
+  extern __shared__ float gst[];           // [G][2] mean, rstd
   const int V = C / 8;
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
   const int Cg = C / G;
   const int Cb = C - Ca;
-  // channel (sum, sumsq) pairs -> LDS with one coalesced pass (all loads in flight at once: a
-  // per-group serial walk of Cg dependent L2 loads cost ~Cg x 0.2 us in every block), then one
-  // thread per group folds its Cg channels from LDS in fp64
-  long long* cst = reinterpret_cast<long long*>(gst + 2 * G);   // [C][2] int64 fixed point
-  for (int c = tid; c < C; c += GN_THREADS) {
-    const long long* src = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
-    cst[2 * c] = src[0];
-    cst[2 * c + 1] = src[1];
-  }
-  __syncthreads();
-  for (int g = tid; g < G; g += GN_THREADS) {
-    long long si = 0, qi = 0;            // exact integer fold of the group's channels
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      si += cst[2 * c];
-      qi += cst[2 * c + 1];
+  // fold the Cg channel (sum, sumsq) pairs of every group straight from global memory with TPG
+  // threads per group (all loads of a thread in flight together), exact int64 sums combined
+  // across the TPG lanes by shuffles, then fp64 mean / rstd.  (The previous prologue staged all
+  // C pairs in LDS and folded each group serially in one thread: Cg = 80 dependent LDS reads per
+  // block at C = 2560, which made the 16^2 / 8^2 applies latency-bound.)
+  const int tpg = G >= GN_THREADS ? 1 : (GN_THREADS / G >= 8 ? 8 : (GN_THREADS / G >= 4 ? 4 : (GN_THREADS / G >= 2 ? 2 : 1)));
+  for (int g0 = 0; g0 < G; g0 += GN_THREADS / tpg) {
+    const int g = g0 + tid / tpg, sub = tid % tpg;
+    long long si = 0, qi = 0;
+    if (g < G) {
+      for (int c = g * Cg + sub; c < (g + 1) * Cg; c += tpg) {
+        const long long* src = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
+        const longlong2 v = *reinterpret_cast<const longlong2*>(src);
+        si += v.x;
+        qi += v.y;
+      }
     }
-    const double s = stat_decode(si, 0), q = stat_decode(qi, 1);
-    const double n = (double)S * Cg;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
-    if (var < 0) var = 0;
-    gst[2 * g] = (float)mean;
-    gst[2 * g + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    for (int o = 1; o < tpg; o <<= 1) {    // tpg lanes of a group are adjacent within one wave
+      si += __shfl_xor(si, o, 64);
+      qi += __shfl_xor(qi, o, 64);
+    }
+    if (g < G && sub == 0) {
+      const double sm = stat_decode(si, 0), q = stat_decode(qi, 1);
+      const double n = (double)S * Cg;
+      const double mean = sm / n;
+      double var = q / n - mean * mean;
+      if (var < 0) var = 0;
+      gst[2 * g] = (float)mean;
+      gst[2 * g + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    }
   }
   __syncthreads();
   const int tv = tid % T, rl = tid / T;
@@ -534,7 +541,7 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long
     if (rpb == step && ((S + rpb - 1) / rpb) * B < 256) rpb = step / 2 >= g.R ? step / 2 : g.R;
   }
   nb = (S + rpb - 1) / rpb;
-  const size_t shs = sizeof(float) * 2 * G + sizeof(long long) * 2 * C;
+  const size_t shs = sizeof(float) * 2 * G;
   if (stats_b == nullptr) Ca = C;
   if (g.VPT == 1)
     hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
