@@ -49,7 +49,9 @@ constexpr int AR_THREADS = 256;        // 4 waves, each owning 16 * RW rows
 // KS = K / 32 k-steps; TI = BNC / 16 W subtiles per chunk; RING = LDS chunk buffers;
 // RW = 16-row A fragments per wave (each W fragment read from LDS feeds RW MFMAs)
 template <int KS, int TI, int RING>
-constexpr int areg_minb() { return RING * 16 * TI * (KS / 2) * 128 <= 80 * 1024 ? 2 : 1; }
+constexpr int areg_minb() {
+  return RING * 16 * TI * (KS / 2) * 128 <= 52 * 1024 ? 3 : (RING * 16 * TI * (KS / 2) * 128 <= 80 * 1024 ? 2 : 1);
+}
 
 // LNK: LayerNorm applied to the A rows already resident in registers (W = W * gamma,
 // bias = bias + W . beta folded offline): row statistics from the fragments, then every
@@ -393,6 +395,7 @@ static int areg_variant() {
 //   v0: 40 KiB chunks, 1 block / CU               v1: 20 KiB chunks, 2 blocks / CU
 //   v2: v1 with 64 rows per wave for gated K = 320 (each LDS W fragment feeds 4 MFMAs, not 2)
 //   v3: v2, and the K = 640 tiles on a 2-deep ring (80 KiB: 2 blocks per CU instead of 1)
+//   v4: v3, and the non-gated K = 320 tiles on a 2-deep ring (40 KiB: 3 blocks per CU)
 // default (-1): v3 (K = 640 ring 2: 585 -> 580 ms/step same box x3, profiles/r2_areg_ring2_ab.txt)
 template <bool LNK>
 void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
@@ -401,13 +404,14 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   if (v < 0) v = 3;
   if (p.K == 320) {
     if (v >= 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
+    else if (v == 4 && !gated) launch_areg_t<10, 2, 2, 2, false, LNK>(p, s);   // 40 KiB: 3 blocks per CU
     else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
     else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
   } else {
     // (the 16-row-chunk variant with the in-kernel LayerNorm gives run-to-run different results
     // at the last bit -- tools/dbg_det_lnk.py; cause not found -- so LNK takes the 32-row chunks)
     // v3: 2-deep ring (80 KiB, 2 blocks per CU) for the 32-row chunks
-    if (v == 3) gated ? launch_areg_t<20, 2, 2, 2, true, LNK>(p, s) : launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
+    if (v >= 3) gated ? launch_areg_t<20, 2, 2, 2, true, LNK>(p, s) : launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
     else if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
     else if (v >= 1 && !LNK) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
     else launch_areg_t<20, 2, 3, 2, false, LNK>(p, s);
