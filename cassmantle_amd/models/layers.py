@@ -72,7 +72,7 @@ class StatsArena:
         if need and self.buf is None:
             self.buf = self._bufs[key] = torch.empty(need, device=x.device, dtype=torch.int64)
         if self.buf is not None:
-            self.buf.zero_()
+            ops.zero_(self.buf)
         self.device = x.device
         return self
 

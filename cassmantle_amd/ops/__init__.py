@@ -622,6 +622,14 @@ def latent_step(eps: torch.Tensor, x: torch.Tensor, hist: torch.Tensor, xs: torc
     ext().latent_step(eps, x, hist, xs, coef, step, unet_in, int(cfg), t0, b0, t1, b1)
 
 
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """In-place zero fill (HIP kernel on the GPU path: no ATen kernel inside a captured step)."""
+    if not _use_hip(t) or not t.is_contiguous() or t.data_ptr() % 16:
+        return t.zero_()
+    ext().zero_(t)
+    return t
+
+
 def advance_step(step: torch.Tensor) -> None:
     if not _use_hip(step):
         step.add_(1)

@@ -536,6 +536,12 @@ void latent_step(const at::Tensor& eps, at::Tensor& x, at::Tensor& hist, at::Ten
 }
 
 void advance_step(at::Tensor& step) { launch_advance_step(step.data_ptr<int>(), cur_stream()); }
+void zero_(at::Tensor& t) {
+  CHECK_DEV(t);
+  CHECK_CONTIG(t);
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, "zero_: 16-byte aligned storage expected");
+  launch_zero(t.data_ptr(), (long long)t.numel() * (long long)t.element_size(), cur_stream());
+}
 
 void softmax_rows(const at::Tensor& S, at::Tensor& P, int64_t causal, const c10::optional<at::Tensor>& kv_lens) {
   CHECK_DEV(S); CHECK_CONTIG(S); CHECK_CONTIG(P);
@@ -653,6 +659,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("timestep_embedding", &timestep_embedding, nogil());
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
+  m.def("zero_", &zero_, nogil());
   m.def("softmax_rows", &softmax_rows, nogil());
   m.def("rms_norm", &rms_norm, nogil());
   m.def("rope_kv", &rope_kv, nogil());

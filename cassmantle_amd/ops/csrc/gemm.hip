@@ -233,7 +233,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
       else if (force_cfg >= kFirstDeep) best.cfg = 12;            // the deep-ring gated tile
-      else if (force_cfg >= kFirstPP) best.cfg = 9;               // the ping-pong gated tile
+      else if (force_cfg >= kFirstPP) best.cfg = force_cfg == 8 ? 8 : 9;   // the ping-pong gated tiles
       return best;
     }
     only = force_cfg;

@@ -529,7 +529,11 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
 template <int CONV>
 void launch_pp_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
   if (is_gated(p.act)) {
-    launch_pp<256, 128, 4, 2, CONV, true>(p, ws, s);   // (256x256 gated spills: 256 VGPRs)
+    // (256x256 gated spills: 256 VGPRs).  cfg 8: 256 x 160 with the 8 waves stacked along M
+    // (wave tile 32 x 160: 5 value/gate pairs), 80 outputs per block -- at M = 2048 x 5120 that
+    // is 512 blocks = 2 full rounds instead of 640 = 2.5 rounds of the 64-output 256 x 128 tile
+    if (p.cfg == 8) launch_pp<256, 160, 8, 1, CONV, true>(p, ws, s);
+    else launch_pp<256, 128, 4, 2, CONV, true>(p, ws, s);
     return;
   }
   switch (p.cfg) {

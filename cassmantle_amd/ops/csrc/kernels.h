@@ -162,5 +162,6 @@ void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, c
                         long long row_bytes0, const void* tab1, void* buf1, long long row_bytes1, int rows,
                         hipStream_t s);
 void launch_advance_step(int* step, hipStream_t s);
+void launch_zero(void* p, long long bytes, hipStream_t s);
 void launch_softmax_rows(const float* S, uint16_t* P, int rows, int cols, int Nq, int causal,
                          const int* kv_lens, hipStream_t s);

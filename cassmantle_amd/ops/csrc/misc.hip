@@ -214,6 +214,14 @@ __global__ void latent_step_kernel(const uint16_t* __restrict__ eps, float* __re
 
 __global__ void advance_step_kernel(int* step) { step[0] += 1; }
 
+// zero-fill with 16-byte vector stores (the GroupNorm statistics slab cleared at the start of
+// every captured UNet step; was an ATen fill kernel inside the graph)
+__global__ void zero_kernel(uint4* __restrict__ p, long long n16, uint8_t* __restrict__ tail, int ntail) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) p[i] = make_uint4(0, 0, 0, 0);
+  if (i < ntail) tail[i] = 0;
+}
+
 // row softmax with optional causal / key-length mask (S fp32 [rows][cols] -> P bf16)
 __global__ void softmax_rows_kernel(const float* __restrict__ S, uint16_t* __restrict__ P, int cols, int Nq,
                                     int causal, const int* __restrict__ kv_lens) {
@@ -392,6 +400,16 @@ void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, c
   const int cb = (int)nblk((long long)r.row_units[0] + r.row_units[1], 256);
   hipLaunchKernelGGL(latent_step_kernel, dim3(lb + cb), dim3(256), 0, s, eps, x, hist, xs, coef, step, unet_in, n,
                      cfg, cin, cstride, lb, r);
+}
+
+void launch_zero(void* p, long long bytes, hipStream_t s) {
+  const long long n16 = bytes / 16;
+  const int ntail = (int)(bytes - n16 * 16);
+  const long long n = n16 > ntail ? n16 : ntail;
+  if (n == 0) return;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(p), n16,
+                     reinterpret_cast<uint8_t*>(p) + n16 * 16, ntail);
 }
 
 void launch_advance_step(int* step, hipStream_t s) {

@@ -95,8 +95,8 @@ class _StepState:
 
     def load(self, x0: torch.Tensor, ctx: torch.Tensor, added: Optional[dict]):
         self.x.copy_(x0)
-        self.xs.zero_()
-        self.hist.zero_()
+        ops.zero_(self.xs)
+        ops.zero_(self.hist)
         self.ctx.copy_(ctx)
         nxt = (x0 * self.plan.c_in0).to(self.unet_in.dtype)
         C = x0.shape[-1]
@@ -111,7 +111,7 @@ class _StepState:
         if added is not None:
             for k, v in added.items():
                 self.added[k].copy_(v)
-        self.step.zero_()
+        ops.zero_(self.step)
 
 
 class StableDiffusion:

@@ -512,11 +512,13 @@ def test_gemm_pp_linear(cfg, M, N, K, split, force_cfg):
 @pytest.mark.parametrize("cfg", PP_CFGS)
 def test_gemm_pp_geglu_cat_stats(cfg, force_cfg):
     force_cfg(cfg)
-    # gated (the planner maps every forced config to the 256x128 gated tile)
-    x = rnd(700, 320, seed=105)
-    w = rnd(2 * 640, 320, scale=320 ** -0.5, seed=106)
-    b = rnd(2 * 640, scale=0.1, seed=107)
-    assert rel_err(ops.linear(x, w, b, act="geglu"), ref.linear(x, w, b, act="geglu")) < 1e-2
+    # gated (the planner maps forced config 8 to the 256x160 8x1-wave gated tile, every other
+    # one to the 256x128 gated tile); N = 360 leaves a partial 80-output block
+    for N_g, seed in ((640, 105), (360, 205)):
+        x = rnd(700, 320, seed=seed)
+        w = rnd(2 * N_g, 320, scale=320 ** -0.5, seed=seed + 1)
+        b = rnd(2 * N_g, scale=0.1, seed=seed + 2)
+        assert rel_err(ops.linear(x, w, b, act="geglu"), ref.linear(x, w, b, act="geglu")) < 1e-2
     # two-source A (channel concatenation) with fused GroupNorm statistics
     B, HW, Ca, Cb, N = 2, 300, 640, 320, 320
     a = rnd(B, HW, Ca, seed=108)
@@ -675,3 +677,16 @@ def test_latent_step_padded_input_and_row_select():
         assert torch.equal(b0, tab0[nxt]) and torch.equal(b1, tab1[nxt])
         assert torch.equal(u8[..., :4], u4) and not u8[..., 4:].any()
     assert torch.equal(x, x4)
+
+
+@pytest.mark.parametrize("n,dtype", [(1, torch.int32), (7, torch.int64), (4099, torch.int64), (12345, torch.float32),
+                                     (33, torch.bfloat16)])
+def test_zero_fill_kernel(n, dtype):
+    """ops.zero_ (HIP zero_kernel: 16-byte stores plus a byte tail) clears exactly the tensor and
+    nothing past it (the StatsArena slab clear inside the captured step)."""
+    big = torch.full((n + 64,), 7, device=DEV, dtype=dtype)
+    t = big[:n]
+    ops.zero_(t)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(big[:n]).item() == 0
+    assert bool((big[n:] == 7).all())
