@@ -370,9 +370,14 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
 bool gemm_areg_ok(const GemmArgs& p) {
   if (p.conv || p.A2 || p.batch != 1 || p.out_f32 || p.ln_rows || p.chan_bias || p.split > 1) return false;
   if (p.ln_wsum && !(p.ln_eps > 0.f)) return false;
-  if (!(p.K == 320 || p.K == 640) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
+  // K = 1280 (16 rows per wave, 160 A registers, 16-row W chunks on a 2-deep ring): the
+  // latency-bound level-3 projections (M = 2048); opt-in while it is being measured
+  static const bool k1280 = [] { const char* e = getenv("CASSMANTLE_AREG_K1280"); return e && e[0] == '1'; }();
+  const bool is1280 = p.K == 1280 && k1280;
+  if (!(p.K == 320 || p.K == 640 || is1280) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
   const bool gated = is_gated(p.act);
-  const int bnc = p.K == 320 ? 64 : 32;
+  if (is1280 && gated) return false;
+  const int bnc = p.K == 320 ? 64 : (p.K == 640 ? 32 : 16);
   if ((gated ? 2 * p.N : p.N) % bnc) return false;
   if (gated && p.stats) return false;
   if (p.stats && (p.stats_hw % 64 != 0)) return false;
@@ -402,6 +407,10 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   const bool gated = is_gated(p.act);
   int v = areg_variant();
   if (v < 0) v = 3;
+  if (p.K == 1280) {
+    launch_areg_t<40, 1, 2, 1, false, LNK>(p, s);
+    return;
+  }
   if (p.K == 320) {
     if (v >= 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
     else if (v == 4 && !gated) launch_areg_t<10, 2, 2, 2, false, LNK>(p, s);   // 40 KiB: 3 blocks per CU
