@@ -37,7 +37,10 @@ struct AttnGeom {
   static constexpr int LDS_BYTES = KT * KSTR * 2 + KT * VSTR * 2;
 };
 
-template <int DQK, int DO, int NW>
+// DB: K/V double-buffered in LDS, so the next tile is stored into the other buffer while this
+// one is read and each tile needs ONE barrier (single buffer: one before the store -- everyone
+// is done reading -- and one after it)
+template <int DQK, int DO, int NW, bool DB>
 // min blocks 8 / NW caps the kernel at 256 registers: the compiler then keeps the MFMA
 // accumulators in VGPRs, where the softmax reads and writes them (with a 512-register budget it
 // chose AGPRs and paid a v_accvgpr_read + write per score per pass: ~144 of ~300 VALU per tile)
@@ -51,6 +54,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   constexpr int VLD = (KT * G::VCH + THREADS - 1) / THREADS;
 
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  constexpr int BUF = KT * G::KSTR + KT * G::VSTR;   // elements of one K/V buffer
   uint16_t* Ks = lds;
   uint16_t* Vs = lds + KT * G::KSTR;
 
@@ -156,18 +160,18 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
       vr[i] = v;
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int bo) {   // bo: element offset of the target buffer
 #pragma unroll
     for (int i = 0; i < KLD; ++i)
-      if (k_lds[i] >= 0) *reinterpret_cast<uint4*>(Ks + k_lds[i]) = kr[i];
+      if (k_lds[i] >= 0) *reinterpret_cast<uint4*>(Ks + bo + k_lds[i]) = kr[i];
 #pragma unroll
     for (int i = 0; i < VLD; ++i)
-      if (v_lds[i] >= 0) *reinterpret_cast<uint4*>(Vs + v_lds[i]) = vr[i];
+      if (v_lds[i] >= 0) *reinterpret_cast<uint4*>(Vs + bo + v_lds[i]) = vr[i];
   };
 
   if (ntiles > 0) {
     gload(0);
-    lstore();
+    lstore(0);
   }
   __syncthreads();
 
@@ -179,6 +183,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
     if (more) gload(t + 1);
+    const int bo = DB ? (t & 1) * BUF : 0;   // this tile's buffer
 
     // ---- S^T = K Q^T for 64 keys (two 32-key accumulators)
     f32x16_t sacc[2];
@@ -186,7 +191,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[hf][r] = MF ? 0.f : -m_run;   // S - m folded into the MFMA
-      const uint16_t* krow = Ks + (hf * 32 + ql) * G::KSTR + 8 * hlf;
+      const uint16_t* krow = Ks + bo + (hf * 32 + ql) * G::KSTR + 8 * hlf;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
@@ -286,7 +291,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     for (int kk = 0; kk < 4; ++kk) {
 #pragma unroll
       for (int dc = 0; dc < NDC; ++dc) {
-        const uint16_t* base = Vs + (16 * kk + tr_row) * G::VSTR + 32 * dc + tr_col;
+        const uint16_t* base = Vs + bo + (16 * kk + tr_row) * G::VSTR + 32 * dc + tr_col;
         s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) s16x4_t*)(base));
         s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -298,10 +303,17 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
       }
     }
 
-    __syncthreads();
-    if (more) {
-      lstore();
+    if constexpr (DB) {
+      // the other buffer was last read in tile t - 1, which every wave finished before the
+      // previous barrier
+      if (more) lstore(BUF - bo);
       __syncthreads();
+    } else {
+      __syncthreads();
+      if (more) {
+        lstore(0);
+        __syncthreads();
+      }
     }
   }
 
@@ -341,7 +353,22 @@ void launch_t(const AttnArgs& a, hipStream_t s) {
   constexpr int QB = 32 * NW;
   int nqb = (a.Nq + QB - 1) / QB;
   dim3 grid(nqb * a.H * a.B);
-  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DO, NW>), grid, dim3(64 * NW), G::LDS_BYTES, s, a);
+  // CASSMANTLE_ATTN_DB=0|1: single / double-buffered K/V (A/B knob; double by default: level-1
+  // self-attention 247 -> 240 us, 568.7 -> 566.7 ms/step same box x3, profiles/r2_attn_db_ab.txt)
+  static const int db = [] { const char* e = getenv("CASSMANTLE_ATTN_DB"); return e ? atoi(e) : 1; }();
+  if (db) {
+    auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true>;
+    if constexpr (2 * G::LDS_BYTES > 65536) {
+      // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+      static const bool once = [&] {
+        (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G::LDS_BYTES);
+        return true;
+      }();
+      (void)once;
+    }
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 2 * G::LDS_BYTES, s, a);
+  } else
+    hipLaunchKernelGGL((attn_fwd_kernel<DQK, DO, NW, false>), grid, dim3(64 * NW), G::LDS_BYTES, s, a);
 }
 
 template <int DQK, int DO>
