@@ -883,6 +883,7 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 12: return launch_t<128, 128, 2, 2, CONV, false, false, 4, true>(p, ws, s);
       case 13: return launch_t<128, 64, 2, 2, CONV, false, false, 5, true>(p, ws, s);
       case 14: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true>(p, ws, s);
+      case 16: return launch_t<128, 80, 4, 1, CONV, false, false, 4, true>(p, ws, s);
       default: break;
     }
   }
