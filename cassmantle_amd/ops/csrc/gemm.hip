@@ -35,9 +35,11 @@ constexpr int BK = 64;
 //   15: A-in-registers short-K kernel (gemm_areg.hip: K = 320 / 640, W streamed in chunks)
 //   16: 128x80 4w (4x1, wave 32x80) S4: M = 2048 x N = 1280 is exactly 256 tiles, one per CU
 //       (the 128x64 tile's 320 blocks ran as 1.25 rounds; the deep rings are one block per CU)
+//   17 / 18 / 19: 128x64 / 128x128 / 128x160 4w, 2 stages staged through registers (buffer
+//       loads + ds_write instead of LDS-DMA: no DMA issue cost on the small latency-bound tiles)
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 17;
+constexpr int kNumTiles = 20;
 constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
 constexpr int kFirstDeep = 11;
@@ -49,7 +51,8 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {256, 128, 1.00f, 256}, {256, 256, 1.60f, 256}, {256, 160, 1.55f, 256},
                                        {256, 128, 1.45f, 256}, {128, 256, 1.45f, 256}, {128, 160, 1.f, 256},
                                        {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
-                                       {128, 64, 1.f, 256},    {128, 80, 1.f, 256}};
+                                       {128, 64, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 768},
+                                       {128, 128, 1.f, 512},   {128, 160, 1.f, 512}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
