@@ -690,3 +690,31 @@ def test_zero_fill_kernel(n, dtype):
     torch.cuda.synchronize()
     assert torch.count_nonzero(big[:n]).item() == 0
     assert bool((big[n:] == 7).all())
+
+
+def test_ln_gemm_bitwise_stable_under_concurrency():
+    """The in-kernel-LayerNorm A-in-registers GEMM (K = 320, 2 blocks/CU) must give bit-identical
+    results while a 4-wave GEMM runs on a second stream.  Before the fix, 16-row groups came out
+    with different LayerNorm statistics in ~60 % of such runs (profiles/r2_lnk_concurrency_fix.txt,
+    tools/dbg_conc_matrix.py)."""
+    from cassmantle_amd.ops._ext import ext
+    M, K, N = 8192, 320, 960
+    x = (rnd(M, K, seed=301).float() * 2 + 0.5).to(torch.bfloat16)
+    g = (torch.rand(K, generator=torch.Generator().manual_seed(302)) + 0.5).to(torch.bfloat16).to(DEV)
+    b = rnd(K, scale=0.1, seed=303)
+    w = rnd(N, K, scale=K ** -0.5, seed=304)
+    wb = rnd(N, scale=0.1, seed=305)
+    fold = ops.ln_fold(g, b, w, wb)
+    ref_out = ops.ln_linear(x, g, b, 1e-5, w, fold=fold).clone()
+    bgA, bgW = rnd(8192, 2048, seed=306), rnd(2048, 2048, scale=0.02, seed=307)
+    s_bg = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s_bg):
+        for _ in range(20):
+            ext().gemm_set_override(0, 1)          # the 4-wave tile: the aggressor of the bisect
+            ops.linear(bgA, bgW)
+            ext().gemm_set_override(-1, 0)
+    outs = [ops.ln_linear(x, g, b, 1e-5, w, fold=fold) for _ in range(30)]
+    torch.cuda.synchronize()
+    bad = sum(int(not torch.equal(y, ref_out)) for y in outs)
+    assert bad == 0, f"{bad}/30 concurrent runs differ from the quiet result"
