@@ -25,6 +25,12 @@ with torch.no_grad():
         B, N, H, d = [int(v) for v in sys.argv[2:6]]
         q, k, v = rnd(B, N, H, d), rnd(B, N, H, d), rnd(B, N, H, d)
         f = lambda: ops.attention(q, k, v, fp8="force")
+    elif kind == "lngeglu":   # LayerNorm-folded GEGLU projection (A-in-registers kernel)
+        M, N, K = [int(v) for v in sys.argv[2:5]]
+        x = rnd(M, K); g = (torch.rand(K, device="cuda") + 0.5).to(torch.bfloat16); bt = rnd(K, scale=0.1)
+        w = rnd(2 * N, K, scale=K ** -0.5); b = rnd(2 * N, scale=0.1)
+        fold = ops.ln_fold(g, bt, w, b)
+        f = lambda: ops.ln_linear(x, g, bt, 1e-5, w, act="geglu", fold=fold)
     for _ in range(iters):
         f()
     torch.cuda.synchronize()
