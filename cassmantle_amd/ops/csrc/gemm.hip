@@ -40,10 +40,13 @@ constexpr int BK = 64;
 //   20: ping-pong 128x160 (4x2 waves, wave 32x80): twice the blocks of 256x160 without split-K
 //       (M = 8192 x N = 640: 256 tiles)
 //   21: ping-pong 128x128 (4x2 waves, wave 32x64, 64 KiB LDS: 2 blocks per CU)
+//   22 / 23: ping-pong 128x64 / 256x64 (4x2 waves, 48 / 80 KiB LDS)
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 22;
+constexpr int kNumTiles = 24;
 constexpr int kPP128 = 20, kPP128x128 = 21;
+// ping-pong configs outside the 7..10 block (dispatch and eligibility)
+constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22 || c == 23; }
 constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
 constexpr int kFirstDeep = 11;
@@ -57,7 +60,7 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 768},
                                        {128, 128, 1.f, 512},   {128, 160, 1.f, 512},   {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 512}};
+                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
@@ -225,7 +228,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     // a table entry is only taken if the kernel family can run this call (same checks as a
     // forced config), so a stale table never selects an unsupported path
     const bool elig = tp.cfg < kFirstPP ||
-                      ((tp.cfg < kFirstDeep || tp.cfg == kPP128 || tp.cfg == kPP128x128) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p) : deep_ok(p)));
+                      (is_pp_cfg(tp.cfg) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p) : deep_ok(p)));
     if (have && elig) return tp;
   }
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
@@ -240,7 +243,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   if (force_cfg == kAreg) {
     if (gemm_areg_ok(p)) return GemmPlan{kAreg, 1};
   } else if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
-      (force_cfg < kFirstPP || ((force_cfg < kFirstDeep || force_cfg == kPP128 || force_cfg == kPP128x128) ? pp_elig : deep_elig))) {
+      (force_cfg < kFirstPP || (is_pp_cfg(force_cfg) ? pp_elig : deep_elig))) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
       else if (force_cfg >= kFirstDeep) best.cfg = 12;            // the deep-ring gated tile
@@ -308,7 +311,7 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     launch_gemm_areg(p, s);
     return;
   }
-  if (((p.cfg >= kFirstPP && p.cfg < kFirstDeep) || p.cfg == kPP128 || p.cfg == kPP128x128) && pp_ok(p)) {
+  if (is_pp_cfg(p.cfg) && pp_ok(p)) {
     if (!p.conv) gemm_pp_c0_launch(p, ws, s);
     else gemm_pp_c2_launch(p, ws, s);
     return;

@@ -542,6 +542,8 @@ void launch_pp_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
     case 10: launch_pp<128, 256, 2, 4, CONV, false>(p, ws, s); break;
     case 20: launch_pp<128, 160, 4, 2, CONV, false>(p, ws, s); break;
     case 21: launch_pp<128, 128, 4, 2, CONV, false>(p, ws, s); break;
+    case 22: launch_pp<128, 64, 4, 2, CONV, false>(p, ws, s); break;
+    case 23: launch_pp<256, 64, 4, 2, CONV, false>(p, ws, s); break;
     default: launch_pp<256, 256, 4, 2, CONV, false>(p, ws, s); break;
   }
 }
