@@ -312,9 +312,15 @@ class UNet(nn.Module):
         for m in ca:
             m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
             if fp8 and m.head_dim == 64 and ops._use_hip(buf):
+                # one e4m3 image per context shape, like the bf16 K/V above: a denoise graph
+                # captured at another batch size keeps pointing at its own image, which is
+                # refilled in place and never freed (a single shared image was
+                # reallocated on a batch-size change under a live graph)
                 kv = m._kv.view(buf.shape[0], buf.shape[1], 2, m.heads, m.head_dim)
-                old = m._kv8 if m._kv8 is not None and m._kv8.device == buf.device else None
-                m._kv8 = ops.pack_kv_fp8(kv[:, :, 0], kv[:, :, 1], out=old)
+                bufs8 = m.__dict__.setdefault("_kv8_bufs", {})
+                k8 = (key, str(buf.device))
+                m._kv8 = ops.pack_kv_fp8(kv[:, :, 0], kv[:, :, 1], out=bufs8.get(k8))
+                bufs8[k8] = m._kv8
             else:
                 m._kv8 = None
 

@@ -137,6 +137,34 @@ def test_sdxl_unet_reduced_depth_full_width(fp8):
     assert c >= (0.995 if fp8 else 0.999), c
 
 
+def test_fp8_cross_kv_survives_batch_size_change_under_graphs():
+    """the e4m3 cross-attention K/V image must be kept per context shape.  A
+    graph captured at B=1, then a generation at B=2, then a replay at B=1 must give exactly the
+    first B=1 image (the B=1 graph keeps reading its own, refilled, K/V image) and match eager."""
+    import dataclasses
+    from cassmantle_amd.models.schedulers import make_plan  # noqa: F401
+    from cassmantle_amd.models.unet import TINY_UNET
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    unet = dataclasses.replace(TINY_UNET, block_out_channels=(64, 128), heads=(1, 2), head_dim=64,
+                               cross_attention_dim=32)
+    spec = dataclasses.replace(SPECS["tiny"], name="tiny64", unet=unet)
+    g = StableDiffusion(spec, device="cuda", use_graphs=True, fp8_attention=True, seed=7)
+    e = StableDiffusion(spec, device="cuda", use_graphs=False, fp8_attention=True, seed=7)
+    p1, p2 = ["a lantern"], ["an ember", "a tower"]
+    a = g.generate_tensor(p1, "blurry", [3], steps=4).clone()
+    lat_a = g.last_latents.float().clone()
+    g.generate_tensor(p2, "blurry", [4, 5], steps=4)
+    torch.cuda.synchronize()
+    c = g.generate_tensor(p1, "blurry", [3], steps=4).clone()
+    lat_c = g.last_latents.float().clone()
+    e.generate_tensor(p1, "blurry", [3], steps=4)
+    lat_e = e.last_latents.float().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, c)
+    assert torch.equal(lat_a, lat_c)
+    assert torch.allclose(lat_a, lat_e, atol=2e-2, rtol=2e-2), (lat_a - lat_e).abs().max()
+
+
 def test_sd15_end_to_end_graph_vs_fp32_reference():
     """a whole 4-step generation (CLIP encode -> graph-replayed denoise -> VAE decode -> uint8)
     vs the same pipeline on the fp32 reference path: the images must agree, not just the shape"""
@@ -155,7 +183,8 @@ def test_sd15_end_to_end_graph_vs_fp32_reference():
     d = np.abs(img.astype(np.float32) - ref.astype(np.float32))
     psnr = 10 * np.log10(255.0 ** 2 / max(float((d ** 2).mean()), 1e-9))
     print(f"[e2e] psnr {psnr:.2f} dB, mean |diff| {d.mean():.3f}")
-    assert psnr > 28.0 and d.mean() < 6.0, (psnr, d.mean())
+    # measured 42.7 dB (round 2); 38 dB leaves ~5 dB for kernel-order rounding changes
+    assert psnr >= 38.0 and d.mean() < 2.0, (psnr, d.mean())
 
 
 def test_unet_is_bit_deterministic_run_to_run():
