@@ -209,7 +209,9 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
 
     @app.get("/healthz")
     async def healthz():
-        return {"ok": True, **service.stats(), "stages": TRACER.snapshot()}
+        sup = getattr(app.state, "supervisor", None)       # supervised multi-GPU worker group
+        extra = {"workers": sup.status()} if sup is not None else {}
+        return {"ok": True, **service.stats(), "stages": TRACER.snapshot(), **extra}
 
     @app.get("/metrics")
     async def metrics():

@@ -70,6 +70,11 @@ class GameConfig:
     metrics_enabled: bool = False
     num_rooms: int = 1
     snapshot_path: Optional[str] = None   # JSON snapshot at round boundaries
+    # --- multi-GPU serving ---
+    # gpus > 1 without torchrun: the front-end supervises one worker process per GPU
+    # (parallel/supervisor.py): a dead / wedged GPU is retired and the rooms re-sharded over the
+    # survivors.  Under torchrun the legacy layout (front-end inside rank 0) is used instead.
+    gpus: int = 1
     # --- multi-GPU failure handling (parallel/rooms.py; reference analog: 120 s lock TTL) ---
     rank_heartbeat_s: float = 1.0         # period of every rank's heartbeat in the PG store
     rank_stale_s: float = 30.0            # a heartbeat older than this marks the rank dead

@@ -91,26 +91,66 @@ STOP = "__stop__"
 
 
 class RankWorker:
-    """Executes generation rounds; identical code on every rank."""
+    """Executes generation rounds; identical code on every rank.
+
+    Data plane: a generator that can return its images ON THE DEVICE
+    (``generate_device``, the SD pipeline) hands them to the gather without any host round trip:
+    the uint8 images stay in HBM, a dedicated COMM stream waits on the pipeline's "decoded" event
+    and runs the gather to rank 0 there (never on the generation stream, never an all-gather: only
+    the front-end rank needs the images), and rank 0 makes ONE device-to-host copy of the whole
+    round.  Host-returning generators (placeholder / remote, the CPU tests) take the same path with
+    CPU tensors.  ``last_gather_us`` is this rank's device time of the round's gather."""
 
     def __init__(self, ctx: DistContext, generator: ImageGenerator, sharding: RoomSharding,
-                 negative_prompt: str = "blurry, distorted, fake, abstract, negative") -> None:
+                 negative_prompt: str = "blurry, distorted, fake, abstract, negative", on_local_done=None) -> None:
         self.ctx = ctx
         self.gen = generator
         self.sharding = sharding
         self.negative = negative_prompt
         self.res = generator.resolution
         self.rounds = 0
+        self.on_local_done = on_local_done     # callable(round_id): this rank's generation finished
+        self.last_gather_us: Optional[float] = None
+        self._comm: Optional["torch.cuda.Stream"] = None
 
     def _device(self) -> torch.device:
         return self.ctx.device if self.ctx.backend == "nccl" else torch.device("cpu")
 
-    def run_round(self, jobs: Optional[List[GenJob]]) -> Optional[Dict[Tuple[str, int], np.ndarray]]:
+    def _comm_stream(self, dev: torch.device):
+        if dev.type != "cuda":
+            return None
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=dev)
+        return self._comm
+
+    def _generate_into(self, mine_jobs: List[GenJob], buf: torch.Tensor, ok: torch.Tensor, comm) -> None:
+        prompts, seeds = [j.prompt for j in mine_jobs], [j.seed for j in mine_jobs]
+        n = len(mine_jobs)
+        gen_dev = getattr(self.gen, "generate_device", None)
+        if gen_dev is not None and comm is not None:
+            out = gen_dev(prompts, self.negative, seeds)          # images stay in HBM
+            comm.wait_event(out.event)                             # ordered after the VAE decode
+            with torch.cuda.stream(comm):
+                out.images.record_stream(comm)
+                buf[:n].copy_(out.images)
+                ok[:n].copy_(out.finite.to(torch.uint8).expand(n) if out.finite is not None else torch.ones_like(ok[:n]))
+            return
+        imgs = self.gen.generate(prompts, self.negative, seeds)
+        host = torch.from_numpy(np.ascontiguousarray(np.stack(imgs)))
+        if comm is not None:
+            with torch.cuda.stream(comm):
+                buf[:n].copy_(host.pin_memory(), non_blocking=True)
+                ok[:n].fill_(1)
+        else:
+            buf[:n].copy_(host)
+            ok[:n] = 1
+
+    def run_round(self, jobs: Optional[List[GenJob]], round_id: int = 0) -> Optional[Dict[Tuple[str, int], np.ndarray]]:
         """Collective: every rank must call it.  Rank 0 passes the job list (or STOP); others
         pass None.  Returns {(room, job_index): image} on rank 0, None elsewhere; returns the
         string STOP on every rank when the loop should end."""
-        msg = broadcast_object((jobs, self.sharding.state()) if self.ctx.rank == 0 else None)   # C1
-        jobs, dead = msg
+        msg = broadcast_object((jobs, self.sharding.state(), round_id) if self.ctx.rank == 0 else None)   # C1
+        jobs, dead, round_id = msg
         if jobs == STOP:
             return STOP  # type: ignore[return-value]
         if tuple(sorted(self.sharding.dead)) != tuple(dead):
@@ -121,40 +161,66 @@ class RankWorker:
         jmax = max((len(p) for p in per_rank), default=0)
         mine = per_rank[rank]
         dev = self._device()
+        comm = self._comm_stream(dev)
         H = self.res
         buf = torch.zeros((max(jmax, 1), H, H, 3), dtype=torch.uint8, device=dev)
         ok = torch.zeros((max(jmax, 1),), dtype=torch.uint8, device=dev)
+        if comm is not None:
+            comm.wait_stream(torch.cuda.current_stream(dev))      # the zero-fills above
         if mine:
             try:
-                imgs = self.gen.generate([jobs[i].prompt for i in mine], self.negative, [jobs[i].seed for i in mine])
-                for k, im in enumerate(imgs):
-                    t = torch.from_numpy(np.ascontiguousarray(im)) if isinstance(im, np.ndarray) else im
-                    buf[k].copy_(t.to(dev))
-                    ok[k] = 1
+                self._generate_into([jobs[i] for i in mine], buf, ok, comm)
             except Exception as e:  # noqa: BLE001 - a failed rank must still join the collectives
                 log.error("[ERROR] rank %d generation failed: %s", rank, e)
+                if comm is not None:
+                    with torch.cuda.stream(comm):
+                        ok.zero_()
+                else:
+                    ok.zero_()
+        if self.on_local_done is not None:
+            self.on_local_done(round_id)
         out = None
-        if W > 1:
-            if rank == 0:
-                gl = [torch.empty_like(buf) for _ in range(W)]
-                gk = [torch.empty_like(ok) for _ in range(W)]
-                dist.gather(buf, gl, dst=0)                                             # C2
-                dist.gather(ok, gk, dst=0)
+        ev0 = ev1 = None
+        with (torch.cuda.stream(comm) if comm is not None else _nullctx()):
+            if comm is not None:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record(comm)
+            if W > 1:
+                if rank == 0:
+                    gl = [torch.empty_like(buf) for _ in range(W)]
+                    gk = [torch.empty_like(ok) for _ in range(W)]
+                    dist.gather(buf, gl, dst=0)                                         # C2
+                    dist.gather(ok, gk, dst=0)
+                else:
+                    dist.gather(buf, None, dst=0)
+                    dist.gather(ok, None, dst=0)
+                    gl = gk = None
             else:
-                dist.gather(buf, None, dst=0)
-                dist.gather(ok, None, dst=0)
-                gl = gk = None
+                gl, gk = [buf], [ok]
+            if comm is not None:
+                ev1.record(comm)
+            host_imgs = host_ok = None
+            if rank == 0:
+                allb, allk = torch.stack(gl), torch.stack(gk)
+                if comm is not None:                               # ONE device-to-host copy per round
+                    host_imgs = torch.empty(allb.shape, dtype=torch.uint8, pin_memory=True)
+                    host_ok = torch.empty(allk.shape, dtype=torch.uint8, pin_memory=True)
+                    host_imgs.copy_(allb, non_blocking=True)
+                    host_ok.copy_(allk, non_blocking=True)
+                else:
+                    host_imgs, host_ok = allb, allk
+        if comm is not None:
+            comm.synchronize()
+            self.last_gather_us = ev0.elapsed_time(ev1) * 1e3
+        if W > 1:
             dist.barrier()                                                              # C4
-        else:
-            gl, gk = [buf], [ok]
         if rank == 0:
             out = {}
+            imgs_np, ok_np = host_imgs.numpy(), host_ok.numpy()
             for r in range(W):
-                host = gl[r].cpu().numpy()
-                flags = gk[r].cpu().numpy()
                 for k, i in enumerate(per_rank[r]):
-                    if flags[k]:
-                        out[(jobs[i].room, i)] = host[k]
+                    if ok_np[r, k]:
+                        out[(jobs[i].room, i)] = imgs_np[r, k].copy()
         self.rounds += 1
         return out
 
@@ -163,6 +229,14 @@ class RankWorker:
         while True:
             if self.run_round(None) == STOP:
                 return
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class GenerationCoordinator:
@@ -185,6 +259,7 @@ class GenerationCoordinator:
         self._inflight: List[cf.Future] = []
         self._mu = threading.Lock()
         self._q: "queue.Queue" = queue.Queue()
+        self._round_id = 0
         self._thread = threading.Thread(target=self._loop, name="gen-coordinator", daemon=True)
         self._stopped = False
         self._thread.start()
@@ -248,12 +323,15 @@ class GenerationCoordinator:
 
     def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
         fut: cf.Future = cf.Future()
-        if self.degraded is not None:
-            fut.set_exception(ImageGenerationError(f"process group degraded: {self.degraded}"))
-            return fut
+        # the degraded check, the in-flight registration and the enqueue happen under the same
+        # lock degrade() takes, so degrade() either sees this request (and fails it) or the
+        # request sees the degraded flag
         with self._mu:
-            self._inflight.append(fut)
-        self._q.put((room, list(prompts), list(seeds), fut))
+            if self.degraded is None:
+                self._inflight.append(fut)
+                self._q.put((room, list(prompts), list(seeds), fut))
+                return fut
+        fut.set_exception(ImageGenerationError(f"process group degraded: {self.degraded}"))
         return fut
 
     def _loop(self) -> None:
@@ -263,6 +341,10 @@ class GenerationCoordinator:
             item = self._q.get()
             if item is None:
                 break
+            if self.degraded is not None:          # degraded while this thread was blocked
+                if not item[3].done():
+                    item[3].set_exception(ImageGenerationError(f"process group degraded: {self.degraded}"))
+                return
             batch = [item]
             t_end = time.monotonic() + self.window
             while True:
@@ -284,8 +366,9 @@ class GenerationCoordinator:
                 jobs.extend(GenJob(room, p, s) for p, s in zip(prompts, seeds))
                 spans.append((start, len(jobs), room, fut))
             self.round_started = time.monotonic()
+            self._round_id += 1
             try:
-                res = self.worker.run_round(jobs)
+                res = self.worker.run_round(jobs, self._round_id)
                 for s, e, room, fut in spans:
                     imgs = [res.get((room, i)) for i in range(s, e)]
                     if fut.done():

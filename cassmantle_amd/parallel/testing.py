@@ -1,0 +1,55 @@
+"""Fault-injecting worker generators for the supervised-group tests ("fault-injection
+flags in the fake generator (fail / slow / NaN)").  A worker builds one through
+``GroupSupervisor(gen_factory="cassmantle_amd.parallel.testing:stamped_generator")``; the fault is
+configured through the worker environment:
+
+* ``CASSMANTLE_FAULT_SLOT``: the device label (``cpu:1``, ``cuda:3``) whose worker misbehaves;
+* ``CASSMANTLE_FAULT``: ``kill`` (the process exits mid-round, like an OOM kill or a driver
+  crash), ``hang`` (the generation never returns but the process keeps heart-beating, like a
+  wedged GPU kernel), ``fail`` (the generation raises);
+* ``CASSMANTLE_FAULT_TRIGGER``: a file; the fault fires only once it exists.
+
+Every image carries the generating slot's index in its top-left 8x8 block (value
+``40 * (index + 1)``, robust to JPEG), so a test can tell which device drew a room's round.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+from ..game.content import ImageGenerationError, SolidImageGenerator
+
+
+class StampedGenerator(SolidImageGenerator):
+    def __init__(self, slot: str, res: int = 32) -> None:
+        super().__init__(res)
+        self.slot = slot
+        self.index = int(slot.split(":")[1]) if ":" in slot else 0
+        self.fault_slot = os.environ.get("CASSMANTLE_FAULT_SLOT")
+        self.fault_mode = os.environ.get("CASSMANTLE_FAULT")
+        self.trigger = os.environ.get("CASSMANTLE_FAULT_TRIGGER")
+
+    def _armed(self) -> bool:
+        return self.slot == self.fault_slot and bool(self.trigger) and os.path.exists(self.trigger)
+
+    def generate(self, prompts, negative_prompt, seeds):
+        if self._armed():
+            if self.fault_mode == "kill":
+                os._exit(17)
+            if self.fault_mode == "hang":
+                time.sleep(3600)
+            if self.fault_mode == "fail":
+                raise ImageGenerationError("injected failure")
+        out = super().generate(prompts, negative_prompt, seeds)
+        for im in out:
+            im[:8, :8, :] = 40 * (self.index + 1)
+        return out
+
+
+def stamped_generator(cfg, device: str, spec) -> StampedGenerator:
+    return StampedGenerator(spec.slot or device, res=cfg.model.resolution)
+
+
+def slot_of(img) -> int:
+    """Inverse of the stamp: slot index that drew ``img`` (uint8 [H, W, 3])."""
+    return int(round(float(img[:8, :8].mean()) / 40.0)) - 1

@@ -309,6 +309,14 @@ class StableDiffusion:
         return [arr[i].copy() for i in range(arr.shape[0])]
 
 
+@dataclass
+class DeviceImages:
+    """A generation's result left in HBM (multi-GPU data plane, ``parallel.rooms.RankWorker``)."""
+    images: torch.Tensor                  # uint8 [B, H, W, 3] on the device
+    finite: Optional[torch.Tensor]        # device bool scalar: the final latents were finite
+    event: "torch.cuda.Event"             # recorded after the VAE decode on the producing stream
+
+
 class DiffusionImageGenerator(ImageGenerator):
     """Game-layer adapter (``ImageGenerator``) around :class:`StableDiffusion`."""
 
@@ -328,3 +336,13 @@ class DiffusionImageGenerator(ImageGenerator):
 
     def generate(self, prompts, negative_prompt, seeds):
         return self.sd.generate(prompts, negative_prompt, seeds, **self.kw)
+
+    def generate_device(self, prompts, negative_prompt, seeds) -> DeviceImages:
+        """``generate`` without the host copy: the images stay on the device, ordered by the
+        returned event (the caller's stream waits on it; nothing is enqueued on the caller's
+        stream here, see ``StableDiffusion.generate_tensor``)."""
+        with self.sd._lock:
+            img = self.sd.generate_tensor(prompts, negative_prompt, seeds, sync_caller=False, **self.kw)
+            ev = torch.cuda.Event()
+            ev.record(self.sd.out_stream)
+            return DeviceImages(img, self.sd.last_finite, ev)

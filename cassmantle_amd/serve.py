@@ -4,14 +4,20 @@ Single GPU / CPU (reference equivalent of ``uvicorn main:app``)::
 
     python -m cassmantle_amd.serve --port 8000 [--num_rooms 4] [--image_model sd15] ...
 
-Whole node, rooms data-parallel over the GPUs (one process per GPU, RCCL over xGMI)::
+Whole node, rooms data-parallel over the GPUs (one worker process per GPU, RCCL over xGMI),
+supervised by the front-end (``parallel.supervisor``; a dead or wedged GPU is retired and its
+rooms move to the survivors)::
+
+    python -m cassmantle_amd.serve --gpus 8 --num_rooms 8
+
+Legacy layout, the front-end inside rank 0 of a ``torchrun`` group (a dead rank degrades the
+node to rank 0's GPU)::
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m cassmantle_amd.serve --num_rooms 8
 
-Rank 0 runs the HTTP/WebSocket front-end and the game state; every rank (0 included) owns the
-rooms ``i mod W`` and generates their images when rank 0's coordinator opens a generation round
-(``parallel.rooms``).  Any ``GameConfig``/``ModelConfig`` field can be passed as ``--field value``
-or ``CASSMANTLE_FIELD`` in the environment.
+Every worker owns the rooms ``i mod W`` and generates their images when the coordinator opens a
+generation round (``parallel.rooms``).  Any ``GameConfig``/``ModelConfig`` field can be passed as
+``--field value`` or ``CASSMANTLE_FIELD`` in the environment.
 """
 from __future__ import annotations
 
@@ -41,6 +47,8 @@ def main(argv=None) -> int:
     from .api.app import create_app
     from .runtime.factory import build_image_generator, build_service
 
+    if world == 1 and cfg.game.gpus > 1:
+        return _serve_supervised(cfg, args)
     if world == 1:
         app = create_app(build_service(cfg), cfg)
         uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
@@ -109,6 +117,31 @@ def main(argv=None) -> int:
         if coord.degraded is None:
             cdist.shutdown()
     return 0 if coord.degraded is None else 3
+
+
+def _serve_supervised(cfg, args) -> int:
+    """Front-end process + supervised worker group (``parallel.supervisor``).  The group is
+    spawned before this process touches the GPU (the scorer and the blur run here, on GPU 0)."""
+    import uvicorn
+    import torch
+    from .api.app import create_app
+    from .parallel.supervisor import GroupSupervisor, SupervisedImageGenerator
+    from .runtime.factory import build_service
+    n = cfg.game.gpus
+    room_ids = [""] + [str(i) for i in range(1, max(cfg.game.num_rooms, n))]
+    cfg.game.num_rooms = len(room_ids)
+    devices = [f"cuda:{i}" for i in range(n)]
+    sup = GroupSupervisor(cfg, devices, room_ids, round_timeout_s=cfg.game.round_timeout_s,
+                          stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s)
+    sup.wait_ready()
+    svc = build_service(cfg, image_gen_for_room=lambda rid: SupervisedImageGenerator(sup, rid), room_ids=room_ids)
+    app = create_app(svc, cfg)
+    app.state.supervisor = sup
+    try:
+        uvicorn.run(app, host=args.host, port=args.port, ws=WS_PROTOCOL, log_level=args.log_level)
+    finally:
+        sup.close()
+    return 0
 
 
 if __name__ == "__main__":

@@ -1,0 +1,120 @@
+"""Supervised worker groups (parallel/supervisor.py) on CPU with gloo, world size 3: a worker
+killed (or wedged) mid-round costs its device only.  The HTTP front-end keeps answering, the
+round's rooms repeat their content (reference fallback, src/backend.py:211-215), and the next
+rounds are drawn by BOTH survivors in a fresh worker group (reference: any live worker takes
+over once the dead holder's lock expires, src/backend.py:83-87,155-159,206-210)."""
+import asyncio
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from cassmantle_amd.parallel.testing import slot_of
+
+
+def _service(sup, rooms):
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.game.service import GameService
+    from cassmantle_amd.parallel.supervisor import SupervisedImageGenerator
+    from cassmantle_amd.scoring.batcher import BatchingScorer
+    from cassmantle_amd.scoring.wordvec import WordVectorBackend
+    cfg = sup.cfg
+    be = WordVectorBackend(vocab=["lantern", "tower"], vectors=np.eye(2, dtype=np.float32))
+    return GameService(cfg, BatchingScorer(be, cfg.game.min_score),
+                       image_gen_for_room=lambda rid: SupervisedImageGenerator(sup, rid, timeout_s=120),
+                       room_ids=rooms, seed=0)
+
+
+def _cfg(rooms):
+    from cassmantle_amd.config import Config
+    cfg = Config()
+    cfg.game.rate_limit_enabled = False
+    cfg.game.max_retries = 1
+    cfg.game.num_rooms = len(rooms)
+    cfg.model.resolution = 32
+    return cfg
+
+
+@pytest.mark.parametrize("fault", ["kill", "hang"])
+def test_dead_worker_retired_survivors_take_over(fault):
+    from fastapi.testclient import TestClient
+    from cassmantle_amd.api.app import create_app
+    from cassmantle_amd.game.imaging import decode_jpeg
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1", "2", "3", "4", "5"]
+    slots = ["cpu:0", "cpu:1", "cpu:2"]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault")
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:1", "CASSMANTLE_FAULT": fault, "CASSMANTLE_FAULT_TRIGGER": trig}
+        sup = GroupSupervisor(_cfg(rooms), slots, rooms, gen_factory="cassmantle_amd.parallel.testing:stamped_generator",
+                              window_s=0.3, round_timeout_s=8.0, stale_s=10.0, worker_env=env,
+                              start_timeout_s=240)
+        try:
+            assert sup.wait_ready(240)
+            svc = _service(sup, rooms)
+            client = TestClient(create_app(svc, sup.cfg, run_timers=False))
+
+            def drawn_by():
+                return {r: slot_of(decode_jpeg(svc.room(r).store.hget(svc.room(r).k("image"), "current")))
+                        for r in rooms}
+
+            def versions():
+                return {r: svc.room(r).store.hget(svc.room(r).k("image"), "version") for r in rooms}
+
+            async def next_round():
+                ok = await asyncio.gather(*(svc.room(r).buffer_contents() for r in rooms))
+                for r in rooms:
+                    await svc.room(r).end_round()
+                return list(ok)
+
+            with client:                                      # startup: round 1 on all three workers
+                start = drawn_by()
+                assert sorted(set(start.values())) == [0, 1, 2], start
+                assert {r for r, s in start.items() if s == 1} == {"1", "4"}
+                v1 = versions()
+                open(trig, "w").close()                        # cpu:1 misbehaves from its next round
+                ok2 = client.portal.call(next_round)
+                v2 = versions()
+                repeated = {r for r in rooms if v2[r] == v1[r]}
+                assert not all(ok2) and repeated >= {"1", "4"}, (ok2, repeated)
+                # the front-end never stopped answering
+                assert [client.get(f"/fetch/contents?room={r}").status_code for r in rooms] == [200] * 6
+                assert [client.get(f"/client/status?room={r}").status_code for r in rooms] == [200] * 6
+                ok3 = client.portal.call(next_round)
+                v3 = versions()
+                after = drawn_by()
+            st = sup.status()
+        finally:
+            sup.close()
+    assert all(ok3) and all(v3[r] != v2[r] for r in rooms), (ok3, v2, v3)
+    assert set(after.values()) == {0, 2}, after                # BOTH survivors draw the next round
+    assert list(st["retired"]) == ["cpu:1"] and st["live_devices"] == ["cpu:0", "cpu:2"], st
+    assert st["epoch"] == 2 and st["failures"][0]["retired"] == ["cpu:1"], st
+
+
+def test_generation_failure_on_one_worker_keeps_group():
+    """a generator that RAISES (no crash, no hang) fails only its own rooms; the group stays up"""
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1", "2", "3"]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault")
+        open(trig, "w").close()
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:1", "CASSMANTLE_FAULT": "fail", "CASSMANTLE_FAULT_TRIGGER": trig}
+        sup = GroupSupervisor(_cfg(rooms), ["cpu:0", "cpu:1"], rooms,
+                              gen_factory="cassmantle_amd.parallel.testing:stamped_generator", window_s=0.3,
+                              worker_env=env, start_timeout_s=240)
+        try:
+            assert sup.wait_ready(240)
+            futs = {r: sup.submit(r, [f"p{r}"], [1]) for r in rooms}
+            res = {}
+            for r, f in futs.items():
+                try:
+                    res[r] = slot_of(f.result(timeout=120)[0])
+                except Exception as e:  # noqa: BLE001
+                    res[r] = type(e).__name__
+            st = sup.status()
+        finally:
+            sup.close()
+    assert res == {"": 0, "1": "ImageGenerationError", "2": 0, "3": "ImageGenerationError"}, res
+    assert st["epoch"] == 1 and not st["retired"] and st["gather_us_p50"] is None
