@@ -6,8 +6,10 @@ GPU, SD-1.5 512×512, 50 PNDM steps (51 UNet evaluations, SD-1.5's default sched
 classifier-free guidance 7.5 (UNet batch 2×4), batch = 4 images per room, bf16, random-init
 weights, synthetic ``seeds.txt`` story prompts.  One benchmark *step* = every rank generates
 its room's 4 images end to end (CLIP encode → hipGraph-replayed denoise loop → VAE decode →
-uint8) and the images are all-gathered to rank 0 over RCCL (what the front-end does at a
-round boundary).  Whole-job images/s = N·4·K / max-over-ranks(time of K steps).
+uint8) and the images are GATHERED to rank 0 over RCCL (C2: what the front-end needs at a round
+boundary; device-resident, on a dedicated comm stream fenced by the decode event, no host hop).
+Whole-job images/s = N·4·K / max-over-ranks(time of K steps); ``per_rank`` reports each rank's
+step time and device time of its gather (µs).
 
 Rank 0 also measures the streaming guess scorer (BASELINE config 1/5): MiniLM-L6 embed +
 cosine for a 64-player micro-batch, p50 latency in ms (reported as ``p50_score_ms``).
@@ -137,28 +139,38 @@ def main() -> int:
 
     H = spec.resolution
     gather_buf = None
-
     gather_ms = []
+    comm = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+    # gloo (the one-GPU multi-rank rehearsal) gathers host tensors; RCCL gathers in HBM
+    host_gather = world > 1 and dist.get_backend() == "gloo"
 
     def one_step(step: int):
         nonlocal gather_buf
         prompts = room_prompts(step)
         seeds = [1000 * rank + 10 * step + j for j in range(args.batch)]
-        # sync_caller=False: the next step's encode + denoise start while this step's VAE decode
-        # still runs on the pipeline's decode stream (stage overlap); the timed region still
-        # ends with a device-wide synchronize
+        # sync_caller=False: nothing is enqueued on this thread's stream; the images are ordered
+        # on the pipeline's output stream only
         img = sd.generate_tensor(prompts, negative, seeds, steps=args.denoise_steps, scheduler=args.scheduler,
                                  sync_caller=False)
-        if world > 1:
-            cur = torch.cuda.current_stream(device)
-            cur.wait_stream(sd.out_stream)
-            img.record_stream(cur)
-            if gather_buf is None:
+        if world > 1 and comm is None:                      # CPU rehearsal (gloo)
+            if gather_buf is None and rank == 0:
                 gather_buf = [torch.empty_like(img) for _ in range(world)]
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            dist.all_gather(gather_buf, img.contiguous())      # C2: images to the front-end rank
-            e1.record()
+            dist.gather(img, gather_buf if rank == 0 else None, dst=0)
+        elif world > 1:
+            # C2 on the comm stream, fenced by the decode event: the next step's encode/denoise
+            # on the generation stream is not ordered behind the collective
+            ev = torch.cuda.Event()
+            ev.record(sd.out_stream)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                img.record_stream(comm)
+                src = img.cpu() if host_gather else img
+                if gather_buf is None and rank == 0:
+                    gather_buf = [torch.empty_like(src) for _ in range(world)]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(comm)
+                dist.gather(src, gather_buf if rank == 0 else None, dst=0)
+                e1.record(comm)
             gather_ms.append((e0, e1))
         return img
 
@@ -186,12 +198,12 @@ def main() -> int:
     elapsed = float(t.item())
     per_rank = None
     if world > 1:
-        # per-rank step time and all-gather (RCCL over xGMI) time, gathered to rank 0
-        ag = [a.elapsed_time(b) for a, b in gather_ms[args.warmup:]] or [0.0]
-        mine_t = torch.tensor([mine / args.steps * 1e3, float(np.mean(ag))], dtype=torch.float64, device=device)
+        # per-rank step time and device time of its image gather (C2, RCCL over xGMI), to rank 0
+        ag = [a.elapsed_time(b) for a, b in gather_ms[args.warmup:]] or [0.0]   # ms
+        mine_t = torch.tensor([mine / args.steps * 1e3, float(np.mean(ag)) * 1e3], dtype=torch.float64, device=device)
         allv = [torch.zeros_like(mine_t) for _ in range(world)]
         dist.all_gather(allv, mine_t)
-        per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "all_gather_ms": round(float(v[1]), 3)}
+        per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "gather_us": round(float(v[1]), 1)}
                     for i, v in enumerate(allv)]
     # batch-1 latency: one room's single image end to end (prompt -> uint8 on host), what a
     # serving room waits on; one warm-up generation (graph capture for batch 1), then 2 timed

@@ -24,6 +24,7 @@ of the client (static/spell.js, reference Typo.js check/suggest) on the server (
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 import base64
 import contextlib
 import logging
@@ -129,6 +130,8 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
             if session_id:
                 room.remove_connection(session_id)
 
+    spell_pool = concurrent.futures.ThreadPoolExecutor(2, thread_name_prefix="spell")
+
     @app.get("/spell")
     async def spell(request: Request, word: str = ""):
         """server twin of the client's affix spell check (game/spell.py == static/spell.js)"""
@@ -138,7 +141,10 @@ def create_app(service: GameService, cfg: Optional[Config] = None, run_timers: b
         w = word.strip()[:32]
         if not w.isalpha():
             return JSONResponse({"word": w, "ok": False, "suggestions": []})
-        return JSONResponse(await asyncio.to_thread(spell_report, w, 5))
+        # a small executor of its own: suggestion searches never queue in front of the
+        # /fetch/contents blur + JPEG work on asyncio's default executor
+        loop = asyncio.get_running_loop()
+        return JSONResponse(await loop.run_in_executor(spell_pool, spell_report, w, 5))
 
     @app.get("/client/status")
     async def check_status(request: Request, session_id: Optional[str] = Cookie(None)):

@@ -67,9 +67,9 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     # fragments; past the default limit the unroller gives up and the accumulators go to scratch
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result", "-Wno-unused-variable",
               "-mllvm", "-pragma-unroll-threshold=100000"]
-    # per-file extra flags.  gemm_areg: no SLP vectorisation (no packed-fp32 v_pk_* VALU in the
-    # in-kernel LayerNorm and the epilogues; see the LNK block of gemm_areg.hip)
-    file_flags = {"gemm_areg.hip": ["-fno-slp-vectorize"]}
+    # per-file extra flags (none: the in-kernel LayerNorm's permlane hazard is padded in the
+    # source, gemm_areg.hip sum_row_groups, instead of by building that file without SLP)
+    file_flags: dict = {}
     cmds = []
     objs = []
     for src in hip_srcs:

@@ -68,6 +68,18 @@ class AffixSpeller:
             self.flags[stem] = self.flags.get(stem, "") + fl
         self.sfx = [r for r in self.rules if r.kind == "SFX"]
         self.pfx = [r for r in self.rules if r.kind == "PFX"]
+        # rules indexed by their affix string: a rule whose affix is not at the word's end
+        # (start) cannot undo it, so check() only tries the few that can (same answers as
+        # scanning every rule; ADVICE r2: distance-2 suggestions ran ~200k full scans)
+        self._sfx_by_add: Dict[str, List[AffixRule]] = {}
+        self._pfx_by_add: Dict[str, List[AffixRule]] = {}
+        for r in self.sfx:
+            self._sfx_by_add.setdefault(r.add, []).append(r)
+        for r in self.pfx:
+            self._pfx_by_add.setdefault(r.add, []).append(r)
+        self._sfx_lens = sorted({len(a) for a in self._sfx_by_add})
+        self._pfx_lens = sorted({len(a) for a in self._pfx_by_add})
+        self._check_cache: Dict[str, bool] = {}
 
     @classmethod
     def load(cls, prefix: Optional[str] = None) -> "AffixSpeller":
@@ -79,25 +91,41 @@ class AffixSpeller:
         fl = self.flags.get(stem)
         return fl is not None and flag in fl
 
+    def _candidates(self, w: str, by_add, lens, suffix: bool):
+        for L in lens:
+            if L >= len(w):
+                break
+            key = w[len(w) - L:] if suffix else w[:L]
+            yield from by_add.get(key, ())
+
     def check(self, word: str) -> bool:
         w = word.strip().lower()
         if not w:
             return False
+        hit = self._check_cache.get(w)
+        if hit is None:
+            hit = self._check(w)
+            if len(self._check_cache) > (1 << 20):
+                self._check_cache.clear()
+            self._check_cache[w] = hit
+        return hit
+
+    def _check(self, w: str) -> bool:
         if w in self.flags:
             return True
-        for r in self.sfx:
+        for r in self._candidates(w, self._sfx_by_add, self._sfx_lens, True):
             stem = r.undo(w)
             if stem is None:
                 continue
             if self._has(stem, r.flag):
                 return True
             if r.cross:                        # prefix + suffix on one stem
-                for p in self.pfx:
+                for p in self._candidates(stem, self._pfx_by_add, self._pfx_lens, False):
                     if p.cross:
                         s2 = p.undo(stem)
                         if s2 is not None and self._has(s2, p.flag) and self._has(s2, r.flag):
                             return True
-        for p in self.pfx:
+        for p in self._candidates(w, self._pfx_by_add, self._pfx_lens, False):
             stem = p.undo(w)
             if stem is not None and self._has(stem, p.flag):
                 return True

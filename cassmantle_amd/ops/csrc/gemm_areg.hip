@@ -30,15 +30,48 @@ CM_DEVICE void areg_blds16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, int 
 }
 
 // sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (the 4 lanes holding one A row) with the gfx950
-// permlane swaps: pure VALU, no ds_bpermute through the LDS unit.  The in-kernel LayerNorm
-// statistics went wrong under two-stream concurrency with __shfl_xor (see the LNK block)
+// permlane swaps: pure VALU, no ds_bpermute through the LDS unit.
+//
+// The in-kernel LayerNorm race (round 2: whole 16-row fragment groups came out with slightly
+// different LayerNorm statistics, only while a workgroup of another kernel shared the CU; the
+// round-2 "fix" built this file with -fno-slp-vectorize) -- what the round-3 screens showed
+// (tools/race_lnk_{concurrency,rows}.py, profiles/r3_lnk_race_rootcause.txt):
+//   * the failures are confined to the LAST fragment group of a wave (j = RW - 1) and need
+//     packed fp32 (v_pk_add/mul/fma_f32, produced by SLP vectorisation) in the statistics /
+//     normalisation PROLOGUE.  There hipcc pairs the (sum, sum of squares) reductions of that
+//     group into packed ops and reads their results at its one-wait-state minimum
+//     (v_pk_add_f32 v[82:83] ; s_nop 0 ; v_pk_mul_f32 v[82:83], v[82:83] ; s_nop 0 ; v_fma_f32
+//     v84, -v83, v83, v82); in the first group's reductions the same readers sit >= 2
+//     instructions away;
+//   * padding the permlane swaps alone (the first hypothesis, kept below) still failed;
+//   * a prologue in scalar fp32 (scalar_f) with SLP ON for the rest of the kernel (the epilogue
+//     keeps its packed ops) passed every screen: 0 / 1440 concurrent runs of the row screen and
+//     0 / 40 x 10 concurrency arms, where the round-2 source built with SLP failed 1-2 / 40 and
+//     dozens of row-screen iterations on the same box.
+// So the mechanism is a read of a packed-fp32 result that the compiler's hazard padding does
+// not protect under issue contention from a co-resident workgroup (a hardware / hazard-table
+// issue we could bracket but not observe at instruction level); the fix lives in the source:
+// no packed fp32 before the first DMA, plus generously padded swaps.
+CM_DEVICE void permlane16_swap_padded(unsigned& a, unsigned& b) {
+  asm volatile("s_nop 4\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+CM_DEVICE void permlane32_swap_padded(unsigned& a, unsigned& b) {
+  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+// An opaque scalar fp32 value: the SLP vectoriser cannot pair two of these into one packed
+// v_pk_*_f32 instruction (the LayerNorm statistics and normalisation prologue, see above)
+CM_DEVICE float scalar_f(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 CM_DEVICE float sum_row_groups(float v) {
-  const unsigned u = __float_as_uint(v);
-  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // rows (0,0,2,2) | (1,1,3,3)
-  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const unsigned w = __float_as_uint(s);
-  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);   // halves (lo,lo) | (hi,hi)
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  unsigned a0 = __float_as_uint(v), a1 = a0;
+  permlane16_swap_padded(a0, a1);                                          // rows (0,0,2,2) | (1,1,3,3)
+  const float s = __uint_as_float(a0) + __uint_as_float(a1);
+  unsigned b0 = __float_as_uint(s), b1 = b0;
+  permlane32_swap_padded(b0, b1);                                          // halves (lo,lo) | (hi,hi)
+  return __uint_as_float(b0) + __uint_as_float(b1);
 }
 
 template <int N>
@@ -92,7 +125,8 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
       afr[j][ks] = as_bf16x8(v);
     }
   }
-  // ---- LayerNorm row statistics: a row's K values sit in the 4 lanes fr, fr+16, fr+32, fr+48
+  // ---- LayerNorm row statistics: a row's K values sit in the 4 lanes fr, fr+16, fr+32, fr+48.
+  // Scalar fp32 only (scalar_f): see the race note above sum_row_groups.
   float ln_mean[RW], ln_rstd[RW];
   if constexpr (LNK) {
 #pragma unroll
@@ -107,16 +141,16 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float lo = __uint_as_float(w4[e] << 16), hi = __uint_as_float(w4[e] & 0xffff0000u);
-          s1 += lo + hi;
-          s2 = fmaf(lo, lo, fmaf(hi, hi, s2));
+          s1 = scalar_f(s1 + scalar_f(lo + hi));
+          s2 = scalar_f(fmaf(lo, lo, scalar_f(fmaf(hi, hi, s2))));
         }
       }
       s1 = sum_row_groups(s1);
       s2 = sum_row_groups(s2);
-      const float mu = s1 * (1.f / (32 * KS));
-      s2 = fmaxf(s2 * (1.f / (32 * KS)) - mu * mu, 0.f) * (32 * KS);
+      const float mu = scalar_f(s1 * (1.f / (32 * KS)));
+      const float var = scalar_f(fmaxf(scalar_f(s2 * (1.f / (32 * KS))) - scalar_f(mu * mu), 0.f));
       ln_mean[j] = mu;
-      ln_rstd[j] = rsqrtf(s2 * (1.f / (32 * KS)) + p.ln_eps);
+      ln_rstd[j] = scalar_f(rsqrtf(var + p.ln_eps));
     }
     // opaque re-definition of the fragments: otherwise hipcc reuses the statistics pass's
     // unpacked floats here and keeps all K / 4 of them live (spills)
@@ -135,7 +169,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
         float f[8];
         unpack8(__builtin_bit_cast(uint4, afr[j][ks]), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = (f[e] - ln_mean[j]) * ln_rstd[j];
+        for (int e = 0; e < 8; ++e) f[e] = scalar_f((f[e] - ln_mean[j]) * ln_rstd[j]);
         afr[j][ks] = as_bf16x8(pack8(f));
       }
     // Finish the statistics before the first W-chunk LDS-DMA.  Their cross-lane sums are
@@ -417,8 +451,13 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
     else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
     else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
   } else {
-    // (the 16-row-chunk variant with the in-kernel LayerNorm gives run-to-run different results
-    // at the last bit -- tools/dbg_det_lnk.py; cause not found -- so LNK takes the 32-row chunks)
+    // CASSMANTLE_AREG_LNK16=1: the 16-row-chunk variant for the in-kernel LayerNorm too (it gave
+    // run-to-run last-bit differences with the builtin permlane swaps; see sum_row_groups)
+    static const bool lnk16 = [] { const char* e = getenv("CASSMANTLE_AREG_LNK16"); return e && e[0] == '1'; }();
+    if (LNK && lnk16 && !gated) {
+      launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
+      return;
+    }
     // v3: 2-deep ring (80 KiB, 2 blocks per CU) for the 32-row chunks
     if (v >= 3) gated ? launch_areg_t<20, 2, 2, 2, true, LNK>(p, s) : launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
     else if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);

@@ -71,6 +71,8 @@ class ShardedSimilarity(SimilarityBackend):
         self.degraded: Optional[str] = None
         self.rounds = 0
         self.sharded_pairs = 0
+        self.slice_failures = 0                      # consecutive rounds with a failed slice
+        self.max_slice_failures = 3
         self._mu = threading.Lock()                  # one collective round at a time
         self._ex = cf.ThreadPoolExecutor(1, thread_name_prefix="score-collective") if ctx.rank == 0 else None
         self._closed = False
@@ -107,10 +109,32 @@ class ShardedSimilarity(SimilarityBackend):
             parts = [torch.empty_like(buf) for _ in range(W)]
             dist.gather(buf, parts, dst=0, group=self.group)                                       # C3
             self.rounds += 1
-            return torch.cat(parts)[:n].cpu().numpy()
+            out = torch.cat(parts)[:n].cpu().numpy()
+            return self._repair(out, guesses, answers)
         dist.gather(buf, None, dst=0, group=self.group)
         self.rounds += 1
         return None
+
+    def _repair(self, out: np.ndarray, guesses, answers) -> np.ndarray:
+        """A rank whose local scoring raised leaves its slice NaN (the gather must still run):
+        re-score those slices here, and stop sharding after ``max_slice_failures`` rounds in a
+        row with a failed slice (a silently failing rank would otherwise turn 1/W of
+        every sharded batch into min_score)."""
+        W, n = self.ctx.world_size, len(guesses)
+        bad_ranks = []
+        for r in range(W):
+            s, e, _ = shard_bounds(n, W, r)
+            if e > s and not np.all(np.isfinite(out[s:e])):
+                bad_ranks.append(r)
+                out[s:e] = self._score_slice(guesses[s:e], answers[s:e])
+        if bad_ranks:
+            self.slice_failures += 1
+            log.error("[ERROR] scoring slice(s) of rank(s) %s failed; re-scored on rank 0", bad_ranks)
+            if self.slice_failures >= self.max_slice_failures:
+                self.degrade(f"rank(s) {bad_ranks} failed their scoring slice {self.slice_failures} rounds in a row")
+        else:
+            self.slice_failures = 0
+        return out
 
     def degrade(self, reason: str) -> None:
         if self.degraded is None:
