@@ -57,6 +57,7 @@ def scorer_bench(device) -> dict:
     vectors one pair at a time (``src/backend.py:303-317``)."""
     import random
     import numpy as np
+    import torch
     from cassmantle_amd.scoring.wordvec import load_vocab
     from cassmantle_amd.game.scoring import score_pairs
     from cassmantle_amd.scoring.encoder import EncoderBackend
@@ -79,6 +80,22 @@ def scorer_bench(device) -> dict:
     for b in (1, 64, 256):
         p50, p99 = run(b, 50)
         out[f"b{b}"] = {"p50_ms": round(p50, 3), "p99_ms": round(p99, 3)}
+    # the reference-equivalent word-vector scorer (K14 gather + normalise + cosine on the GPU,
+    # ops.gather_cosine; reference: wv.similarity per pair, src/backend.py:303-317), 300-d table
+    # over the 49k-word list (random-init vectors, as BASELINE specifies)
+    from cassmantle_amd.scoring.wordvec import WordVectorBackend
+    be_wv = WordVectorBackend(device=str(device), dtype=torch.bfloat16)
+    wv = {}
+    for b in (1, 64, 256):
+        lat = []
+        for it in range(53):
+            guesses = rng.sample(words, b)
+            pairs = [(g, secrets[i % 2]) for i, g in enumerate(guesses)]
+            t1 = time.perf_counter()
+            score_pairs(be_wv, pairs, 0.01)
+            if it >= 3:
+                lat.append((time.perf_counter() - t1) * 1e3)
+        wv[f"b{b}"] = {"p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3)}
     # CPU baselines (config 1)
     cpu = EncoderBackend(device="cpu")
     lat = []
@@ -96,7 +113,7 @@ def scorer_bench(device) -> dict:
         float(np.dot(a, b) / (np.linalg.norm(a) * np.linalg.norm(b)))
         lat_np.append((time.perf_counter() - t1) * 1e3)
     return {"p50_score_ms": out["b64"]["p50_ms"], "p99_score_ms": out["b64"]["p99_ms"], "score_batch": 64,
-            "score_latency": out, "cpu_minilm_1pair_p50_ms": round(float(np.percentile(lat, 50)), 3),
+            "score_latency": out, "score_latency_wordvec": wv, "cpu_minilm_1pair_p50_ms": round(float(np.percentile(lat, 50)), 3),
             "cpu_numpy_cosine_1pair_p50_ms": round(float(np.percentile(lat_np, 50)), 5)}
 
 

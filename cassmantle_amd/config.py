@@ -110,6 +110,9 @@ class ModelConfig:
     scorer: str = "minilm"               # minilm | wordvec
     scorer_weights: Optional[str] = None  # BertModel / sentence-transformers MiniLM safetensors
     scorer_batch_window_ms: float = 1.0   # micro-batch window for streaming guess scoring
+    # CUs reserved for guess scoring on a GPU that also generates (runtime/cumask.py): the scorer
+    # stream runs on these CUs only, the generation stream on the rest (0 = no reservation)
+    scorer_reserved_cus: int = 0
     prompt_generator: str = "synthetic"   # synthetic | lm | remote
     lm_model: str = "tiny-lm"             # tiny-lm | mistral-7b (models/lm.py)
     lm_weights: Optional[str] = None      # HF-layout safetensors dir/file for the LM

@@ -113,27 +113,34 @@ class Conv2d(nn.Module):
         self.weight = _param((cout, k, k, cin), 1.0 / math.sqrt(cin * k * k), gen, dtype)
         self.bias = _param((cout,), 0.02, gen, dtype) if bias else None
 
-    _w4 = None   # parity-folded 2x2 weights for the upsampling conv (ops.fold_upsample_weights)
-    _w4_key = None
+    # Derived weights are non-persistent BUFFERS keyed by the source weight's version counter:
+    # computed once (StableDiffusion prepares them on the CPU before moving the model, so no
+    # ATen kernel runs on the GPU for them), they follow .to(device), and an in-place weight
+    # load (version bump) recomputes them.
+    upsampling = False   # set by the Upsample blocks: prepare() folds the parity weights
+    pad_in = 0           # channel-padded input width prepare() builds padded weights for
+
+    def _derived(self, name: str, key, fn):
+        buf = self._buffers.get(name)
+        if buf is None or getattr(self, "_key_" + name, None) != key or buf.device != self.weight.device:
+            self.register_buffer(name, fn(), persistent=False)
+            setattr(self, "_key_" + name, key)
+        return self._buffers[name]
 
     def up2_weights(self):
-        """Folded per-parity weights of an upsampling 3x3 conv, refreshed when the weight
-        tensor changes (in-place loads bump its version counter)."""
-        key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
-        if self._w4 is None or self._w4_key != key:
-            self._w4 = ops.fold_upsample_weights(self.weight)
-            self._w4_key = key
-        return self._w4
-
-    _wpad = None   # weight zero-padded to a channel-padded input (UNet conv_in: 4 -> 8 channels)
-    _wpad_key = None
+        """Folded per-parity weights of an upsampling 3x3 conv (ops.fold_upsample_weights)."""
+        return self._derived("w4", self.weight._version, lambda: ops.fold_upsample_weights(self.weight))
 
     def padded_weight(self, cin: int):
-        key = (self.weight.data_ptr(), self.weight._version, cin)
-        if self._wpad is None or self._wpad_key != key:
-            self._wpad = torch.nn.functional.pad(self.weight, (0, cin - self.cin)).contiguous()
-            self._wpad_key = key
-        return self._wpad
+        """Weight zero-padded to a channel-padded input (UNet conv_in: 4 -> 8 channels)."""
+        return self._derived("wpad", (self.weight._version, cin),
+                             lambda: torch.nn.functional.pad(self.weight, (0, cin - self.cin)).contiguous())
+
+    def prepare(self) -> None:
+        if self.upsampling and self.k == 3 and self.cin % 64 == 0:
+            self.up2_weights()
+        if self.pad_in > self.cin:
+            self.padded_weight(self.pad_in)
 
     def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None):
         if x.shape[-1] > self.cin:

@@ -120,10 +120,12 @@ class CLIPTextEncoder(nn.Module):
             if cfg.projection_dim else None
         self.tokenizer = clip_tokenizer(cfg.max_positions, cfg.vocab_size)
 
-    def forward(self, ids: torch.Tensor, output_hidden: int = -1):
-        """ids [B, 77] -> (last/penultimate hidden [B,77,D], pooled [B,P] or None)."""
+    def forward(self, ids: torch.Tensor, output_hidden: int = -1, eos_rows: Optional[torch.Tensor] = None):
+        """ids [B, 77] -> (last/penultimate hidden [B,77,D], pooled [B,P] or None).
+        ``eos_rows`` (int32 [B], = b * 77 + position of the first EOS, built on the host by
+        :meth:`encode`) gathers the pooled rows without a device argmax."""
         B, L = ids.shape
-        x = self.token_embedding[ids] + self.position_embedding[:L][None]
+        x = ops.gather_add(self.token_embedding, ids, self.position_embedding)   # token + position
         hidden = None
         n = len(self.layers)
         for i, blk in enumerate(self.layers):
@@ -135,13 +137,20 @@ class CLIPTextEncoder(nn.Module):
             hidden = last
         pooled = None
         if self.text_projection is not None:
-            eos_pos = (ids == self.tokenizer.eos).int().argmax(dim=1)
-            pooled = self.text_projection(last[torch.arange(B, device=ids.device), eos_pos])
+            if eos_rows is None:
+                eos_pos = (ids == self.tokenizer.eos).int().argmax(dim=1)
+                eos_rows = torch.arange(B, device=ids.device) * L + eos_pos
+            pooled = self.text_projection(ops.gather_add(last.reshape(B * L, -1), eos_rows))
         return hidden, pooled
 
     def encode(self, texts: Sequence[str], device, output_hidden: int = -1):
         ids, _ = self.tokenizer(texts, pad_to=self.cfg.max_positions)
-        return self.forward(ids.to(device), output_hidden)
+        eos_rows = None
+        if self.text_projection is not None:
+            B, L = ids.shape
+            eos_rows = (torch.arange(B) * L + (ids == self.tokenizer.eos).int().argmax(dim=1)).int().to(device)
+        # int32 ids, converted on the host: the embedding gather takes them as they are
+        return self.forward(ids.int().to(device), output_hidden, eos_rows)
 
 
 @dataclass

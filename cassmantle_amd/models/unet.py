@@ -102,9 +102,11 @@ class ResnetBlock(nn.Module):
         return self.conv2(h, residual=sc, stats=s2), s2          # residual fused in epilogue
 
 
-# LayerNorm folded into the following projection GEMM (row-statistics pass + epilogue
-# correction).  Measured neutral on SD-1.5 (684 vs 681 ms/step, profiles/r1_bench_lnfold_ab.jsonl):
-# the read-only statistics pass costs about what the LayerNorm kernel did, so it is opt-in.
+# LayerNorm folded into the following projection GEMM: for K = 320 / 640 (SD-1.5 levels 1-2)
+# the A-in-registers kernel computes the row statistics itself (no LayerNorm kernel, no stats
+# pass; its round-2 concurrency race is fixed in the source, profiles/r3_lnk_race_rootcause.txt);
+# other K take a read-only row-statistics pass + epilogue correction.  On by default;
+# CASSMANTLE_LN_FOLD=0 restores LayerNorm kernel + plain GEMM.
 _LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "1") == "1"
 
 
@@ -118,19 +120,25 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = LayerNorm(dim, 1e-5, dtype)
         self.ff = GEGLUFeedForward(dim, 4, gen=gen, dtype=dtype)
 
-    _folds = None   # LayerNorm-folded projection weights (ops.ln_fold), built on first HIP use
+    _folds = None   # LayerNorm-folded projection weights (ops.ln_fold)
+
+    def _fold_sources(self):
+        return ((self.norm1, self.attn1.to_qkv), (self.norm2, self.attn2.to_q), (self.norm3, self.ff.proj_in))
 
     def folds(self):
-        """(W*gamma, wsum, b + W.beta) of norm1->to_qkv, norm2->to_q, norm3->ff.proj_in.  Reset
-        by UNet.fuse_projections (call it again after loading weights)."""
-        if self._folds is None:
-            self._folds = (ops.ln_fold(self.norm1.weight, self.norm1.bias, self.attn1.to_qkv.weight,
-                                       self.attn1.to_qkv.bias),
-                           ops.ln_fold(self.norm2.weight, self.norm2.bias, self.attn2.to_q.weight,
-                                       self.attn2.to_q.bias),
-                           ops.ln_fold(self.norm3.weight, self.norm3.bias, self.ff.proj_in.weight,
-                                       self.ff.proj_in.bias))
-        return self._folds
+        """(W*gamma, wsum, b + W.beta) of norm1->to_qkv, norm2->to_q, norm3->ff.proj_in, kept as
+        non-persistent buffers (computed once -- on the CPU by UNet.prepare -- and moved with
+        the module); recomputed when a source weight changes (in-place loads bump versions)."""
+        key = tuple((n.weight._version, None if n.bias is None else n.bias._version, l.weight._version,
+                     None if l.bias is None else l.bias._version) for n, l in self._fold_sources())
+        buf = self._buffers.get("fold0_w")
+        if buf is None or self._fold_key != key or buf.device != self.norm1.weight.device:
+            for i, (n, l) in enumerate(self._fold_sources()):
+                for tag, t in zip(("w", "s", "b"), ops.ln_fold(n.weight, n.bias, l.weight, l.bias)):
+                    self.register_buffer(f"fold{i}_{tag}", t, persistent=False)
+            self._fold_key = key
+        return tuple((self._buffers[f"fold{i}_w"], self._buffers[f"fold{i}_s"], self._buffers[f"fold{i}_b"])
+                     for i in range(3))
 
     def forward(self, x, ctx, fp8=False):
         if _LN_FOLD and x.device.type == "cuda" and ops.get_mode() == "hip":
@@ -183,6 +191,7 @@ class Upsample(nn.Module):
     def __init__(self, c: int, gen, dtype):
         super().__init__()
         self.conv = Conv2d(c, c, 3, gen=gen, dtype=dtype)
+        self.conv.upsampling = True
 
     def forward(self, x, arena: Optional[StatsArena] = None):
         so = arena.take(x.shape[0], self.conv.cout) if arena is not None else None
@@ -197,6 +206,7 @@ class UNet(nn.Module):
         ch = cfg.block_out_channels
         g, eps, te = cfg.norm_groups, cfg.norm_eps, cfg.time_embed_dim
         self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, gen=gen, dtype=dtype)
+        self.conv_in.pad_in = 8 if cfg.in_channels % 8 else 0   # the pipeline's channel-padded input
         self.time_linear_1 = Linear(cfg.time_proj_dim, te, gen=gen, dtype=dtype)
         self.time_linear_2 = Linear(te, te, gen=gen, dtype=dtype)
         if cfg.addition_embed:
@@ -246,16 +256,20 @@ class UNet(nn.Module):
 
     # ------------------------------------------------------------------
     def time_embed(self, t: torch.Tensor, added: Optional[dict] = None) -> torch.Tensor:
-        """Returns SiLU(temb) (every consumer applies SiLU first, so it is fused here)."""
-        tp = ops.timestep_embedding(t, self.cfg.time_proj_dim).to(self.time_linear_1.weight.dtype)
-        emb = self.time_linear_2(self.time_linear_1(tp, act="silu"))
-        if self.cfg.addition_embed and added is not None:
-            tid = added["time_ids"]                                  # [B, 6]
-            B = tid.shape[0]
-            te = ops.timestep_embedding(tid.reshape(-1), self.cfg.addition_time_embed_dim).reshape(B, -1)
-            a_in = torch.cat([added["text_embeds"].float(), te], dim=-1).to(emb.dtype)
-            emb = self.add_linear_2(self.add_linear_1(a_in, act="silu"), residual=emb)
-        return _silu(emb)
+        """Returns SiLU(temb) (every consumer applies SiLU first, so it is fused here: into the
+        second time-MLP GEMM's epilogue, or after the SDXL add-embedding residual)."""
+        dt = self.time_linear_1.weight.dtype
+        tp = ops.timestep_embedding(t, self.cfg.time_proj_dim, out_dtype=dt)
+        h = self.time_linear_1(tp, act="silu")
+        if not (self.cfg.addition_embed and added is not None):
+            return self.time_linear_2(h, act="silu")
+        emb = self.time_linear_2(h)
+        tid = added["time_ids"]                                      # [B, 6]
+        B = tid.shape[0]
+        te = ops.timestep_embedding(tid.reshape(-1), self.cfg.addition_time_embed_dim).reshape(B, -1)
+        a_in = ops.concat_last(added["text_embeds"], te)             # [B, 1280 + 1536] in dt
+        emb = self.add_linear_2(self.add_linear_1(a_in, act="silu"), residual=emb)
+        return ops.silu_(emb)
 
     # ------------------------------------------------------------------ fused projections
     def resnets(self) -> List[ResnetBlock]:
@@ -269,9 +283,6 @@ class UNet(nn.Module):
         (22 launch-bound M=B GEMMs per step -> 1) and every cross-attention's context K/V
         projection into ONE [sum 2C, D_ctx] GEMM (run once per generation by
         :meth:`set_context`).  Call again after loading weights."""
-        for blk in self.modules():
-            if isinstance(blk, BasicTransformerBlock):
-                blk._folds = None                                   # re-fold LayerNorms lazily
         rs = self.resnets()
         off = 0
         for r in rs:
@@ -289,6 +300,18 @@ class UNet(nn.Module):
                              persistent=False)
         self._kv_bufs: dict = {}
         self._fused = True
+
+    def prepare(self) -> "UNet":
+        """Compute every derived weight now (fused projection weights, LayerNorm folds,
+        upsampling-conv parity weights, channel-padded conv_in): on the CPU before the model is
+        moved to the GPU, so no setup kernel runs there (they follow .to(device))."""
+        self.fuse_projections()
+        for m in self.modules():
+            if isinstance(m, BasicTransformerBlock):
+                m.folds()
+            elif isinstance(m, Conv2d):
+                m.prepare()
+        return self
 
     def set_context(self, ctx: Optional[torch.Tensor], fp8: bool = False) -> None:
         """Precompute all cross-attention K/V for a (constant) text context.  Buffers are kept
@@ -324,18 +347,26 @@ class UNet(nn.Module):
             else:
                 m._kv8 = None
 
-    def time_table(self, tsteps: torch.Tensor, nb: int, added: Optional[dict] = None):
+    def time_table(self, tsteps: torch.Tensor, nb: int, added: Optional[dict] = None,
+                   t_rep: Optional[torch.Tensor] = None, rep_ids: Optional[torch.Tensor] = None):
         """Time conditioning of a whole denoise schedule at once: SiLU(temb) [E, nb, D] and every
         ResNet's time bias [E, nb, sum Cout] for the E timesteps of a plan.  Both depend only on
         (t, add-embeds), so a sampler computes them with ONE batched MLP + GEMM per generation
-        (E*nb rows) instead of the time MLP and an M=nb weight-streaming GEMV in every step."""
+        (E*nb rows) instead of the time MLP and an M=nb weight-streaming GEMV in every step.
+        ``t_rep`` (f32 [E*nb], row e*nb + b = tsteps[e]) and ``rep_ids`` (int32 [E*nb], = row % nb)
+        let a caller that prebuilt them on the host skip the device-side repeats."""
         if not getattr(self, "_fused", False):
             self.fuse_projections()
         E = tsteps.shape[0]
-        t = tsteps.float().repeat_interleave(nb)                     # row e*nb + b <- tsteps[e]
+        t = t_rep if t_rep is not None else tsteps.float().repeat_interleave(nb)
         rep = None
         if added is not None:
-            rep = {k: v.repeat(E, *([1] * (v.dim() - 1))) for k, v in added.items()}
+            if rep_ids is not None and ops._use_hip(added["text_embeds"]):
+                rep = {"text_embeds": ops.gather_add(added["text_embeds"], rep_ids),
+                       "time_ids": added["time_ids_rep"] if "time_ids_rep" in added
+                       else added["time_ids"].repeat(E, 1)}
+            else:
+                rep = {k: v.repeat(E, *([1] * (v.dim() - 1))) for k, v in added.items() if k != "time_ids_rep"}
         temb = self.time_embed(t, rep)
         tb = ops.linear(temb, self._tb_w, self._tb_b)
         return temb.view(E, nb, -1), tb.view(E, nb, -1)

@@ -82,6 +82,7 @@ class VAEDecoder(nn.Module):
         g, eps = cfg.norm_groups, cfg.eps
         self.post_quant_conv = Conv2d(cfg.latent_channels, cfg.latent_channels, 1, padding=0, gen=gen, dtype=dtype)
         self.conv_in = Conv2d(cfg.latent_channels, ch[0], 3, gen=gen, dtype=dtype)
+        self.conv_in.pad_in = 8 if cfg.latent_channels % 8 else 0   # fed by the 8-channel post-quant GEMM
         self.mid_res1 = VAEResnet(ch[0], ch[0], g, eps, gen, dtype)
         self.mid_attn = VAEAttention(ch[0], g, eps, gen, dtype)
         self.mid_res2 = VAEResnet(ch[0], ch[0], g, eps, gen, dtype)
@@ -94,15 +95,52 @@ class VAEDecoder(nn.Module):
                 blk.resnets.append(VAEResnet(cur, c, g, eps, gen, dtype))
                 cur = c
             blk.upsample_conv = Conv2d(cur, cur, 3, gen=gen, dtype=dtype) if i < len(ch) - 1 else None
+            if blk.upsample_conv is not None:
+                blk.upsample_conv.upsampling = True
             self.up.append(blk)
         self.conv_norm_out = GroupNorm(g, cur, eps, dtype)
         self.conv_out = Conv2d(cur, cfg.out_channels, 3, gen=gen, dtype=dtype)
         self._arena = StatsArena()
 
+    def prepare(self) -> "VAEDecoder":
+        """Derived weights now (on the CPU before the move to the GPU, like UNet.prepare): the
+        upsampling convs' parity weights and the 1/scaling_factor folded into post_quant_conv."""
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                m.prepare()
+        self.pq_scaled()
+        return self
+
+    def pq_scaled(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """post_quant_conv as a GEMM with 1/scaling_factor folded in and its output padded to 8
+        channels (zero rows): conv_in then reads whole 16-byte k-chunks with its padded weight
+        instead of padding its input and weight on every call."""
+        pq = self.post_quant_conv
+        cp = 8 if pq.cout % 8 else pq.cout
+
+        def wfn():
+            w = torch.zeros((cp, pq.cin), dtype=torch.float32, device=pq.weight.device)
+            w[:pq.cout] = pq.weight.float().view(pq.cout, pq.cin) / self.cfg.scaling_factor
+            return w.to(pq.weight.dtype).contiguous()
+
+        def bfn():
+            b = torch.zeros((cp,), dtype=pq.weight.dtype, device=pq.weight.device)
+            if pq.bias is not None:
+                b[:pq.cout] = pq.bias
+            return b
+        key = (pq.weight._version, None if pq.bias is None else pq.bias._version)
+        return pq._derived("wscaled", key, wfn), pq._derived("bpadded", key, bfn)
+
     def forward(self, z: torch.Tensor) -> torch.Tensor:
         """z: scaled latents [B, h, w, 4] NHWC -> image [B, 8h, 8w, 3] in [-1, 1] (model dtype)."""
-        z = (z.float() / self.cfg.scaling_factor).to(self.conv_in.weight.dtype)
-        h = self.post_quant_conv(z)
+        if z.device.type == "cuda" and ops.get_mode() == "hip" and z.dtype == self.conv_in.weight.dtype:
+            # 1/scaling_factor lives in the post_quant_conv weight: no scale / cast launches;
+            # its 8-channel output feeds conv_in's padded weight (no per-call pad copies)
+            w, b = self.pq_scaled()
+            h = ops.linear(z, w, b)
+        else:
+            z = (z.float() / self.cfg.scaling_factor).to(self.conv_in.weight.dtype)
+            h = self.post_quant_conv(z)
         ar = self._arena.begin(tuple(z.shape), z)
         B = z.shape[0]
         hs = ar.take(B, self.conv_in.cout)

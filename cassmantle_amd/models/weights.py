@@ -300,6 +300,8 @@ def load_pipeline_weights(sd_pipe, root: str) -> Dict[str, int]:
             miss = load_state(model, read_safetensors(p), kind, strict=False)
             stats[sub] = len(miss)
     sd_pipe.unet.fuse_projections()   # refresh the fused time-embedding / context-K/V weights
+    if hasattr(sd_pipe, "prepare"):
+        sd_pipe.prepare()             # and the other derived weights (folds, parity convs, ...)
     if len(sd_pipe.text_encoders) > 1 and os.path.exists(os.path.join(root, "text_encoder_2")):
         miss = load_state(sd_pipe.text_encoders[1], read_safetensors(os.path.join(root, "text_encoder_2")), "clip",
                           strict=False)

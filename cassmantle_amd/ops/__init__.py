@@ -108,7 +108,7 @@ STAT_SCALE = (2.0 ** 24, 2.0 ** 16)
 
 def new_stats(B: int, C: int, device) -> torch.Tensor:
     """A zeroed statistics buffer for ``stats=`` arguments: int64 [B, C, 2]."""
-    return torch.zeros((B, C, 2), device=device, dtype=torch.int64)
+    return zero_(torch.empty((B, C, 2), device=device, dtype=torch.int64))
 
 
 def stats_to_float(stats: torch.Tensor) -> torch.Tensor:
@@ -189,6 +189,12 @@ def row_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
     return out
 
 
+# 1: fold every LayerNorm into its projection (row-statistics pass + epilogue correction when the
+# A-in-registers kernel cannot compute the statistics itself); 2: fold only where it can
+# (K = 320 / 640), LayerNorm kernel + plain GEMM elsewhere (A/B knob CASSMANTLE_LN_FOLD_MODE)
+LN_FOLD_MODE = int(os.environ.get("CASSMANTLE_LN_FOLD_MODE", "1"))
+
+
 def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], eps: float,
               w: torch.Tensor, bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               act: Optional[str] = None, fold=None) -> torch.Tensor:
@@ -198,7 +204,7 @@ def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.
     correction — the normalised activation is never written or re-read."""
     K = x.shape[-1]
     rows = x.numel() // K
-    if fold is None or not _use_hip(x) or rows <= 8 or K % 8:
+    if fold is None or not _use_hip(x) or rows <= 8 or K % 8 or (LN_FOLD_MODE == 2 and K not in (320, 640)):
         return linear(layer_norm(x, ln_weight, ln_bias, eps), w, bias, residual=residual, act=act)
     wf, wsum, bf = fold
     x2 = x.reshape(rows, K)
@@ -594,12 +600,76 @@ def vae_postprocess(x: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- diffusion glue (K10/K11)
-def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0,
+                       out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """Sinusoidal embedding [B, dim]; ``out_dtype`` bf16 writes the time MLP's input directly."""
     if not _use_hip(t):
-        return ref.timestep_embedding(t, dim, flip_sin_to_cos, shift)
-    out = torch.empty((t.shape[0], dim), device=t.device, dtype=torch.float32)
-    ext().timestep_embedding(t.float().contiguous(), out, int(flip_sin_to_cos), float(shift))
+        return ref.timestep_embedding(t, dim, flip_sin_to_cos, shift).to(out_dtype)
+    out = torch.empty((t.shape[0], dim), device=t.device, dtype=out_dtype)
+    tf = t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+    ext().timestep_embedding(tf, out, int(flip_sin_to_cos), float(shift))
     return out
+
+
+def gather_add(table: torch.Tensor, ids: torch.Tensor, pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``table[ids] (+ pos[t])`` for ids [B, T] (or [R]) -> [..., D] in table's dtype: the CLIP
+    token + position embedding, or a plain row gather (``pos`` None).  HIP path: int32 ids on
+    the device, one kernel (no ATen index / add)."""
+    if not _use_hip(table):
+        x = table[ids.long()]
+        if pos is not None:
+            x = x + pos[: ids.shape[-1]].view(*([1] * (ids.dim() - 1)), ids.shape[-1], -1)
+        return x
+    D = table.shape[-1]
+    out = torch.empty((*ids.shape, D), device=table.device, dtype=table.dtype)
+    ids32 = ids if ids.dtype == torch.int32 else ids.int()
+    ext().gather_add(table.contiguous(), ids32.contiguous(), pos, int(ids.shape[-1]) if pos is not None else 0, out)
+    return out
+
+
+def concat_last(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``cat([a, b.to(a.dtype)], -1)`` (b bf16 or fp32)."""
+    if not _use_hip(a) or a.dtype != torch.bfloat16 or a.shape[-1] % 8 or b.shape[-1] % 8:
+        return torch.cat([a, b.to(a.dtype)], dim=-1)
+    out = torch.empty((*a.shape[:-1], a.shape[-1] + b.shape[-1]), device=a.device, dtype=a.dtype)
+    ext().concat2(a.contiguous(), b.contiguous(), out)
+    return out
+
+
+def silu_(x: torch.Tensor) -> torch.Tensor:
+    """In-place SiLU (computed in fp32)."""
+    if not _use_hip(x) or x.dtype != torch.bfloat16 or x.numel() % 8 or not x.is_contiguous():
+        x.copy_(torch.nn.functional.silu(x.float()).to(x.dtype))
+        return x
+    ext().silu_(x)
+    return x
+
+
+def latent_init(x0: torch.Tensor, c_in0: float, x: torch.Tensor, xs: torch.Tensor, hist: torch.Tensor,
+                unet_in: torch.Tensor, cfg: bool) -> None:
+    """Start of a generation: x = x0, xs = hist = 0, UNet input (both CFG halves) = c_in0 * x0
+    in the channel-padded bf16 layout (padding channels stay as they are: zero)."""
+    if not _use_hip(x):
+        x.copy_(x0)
+        xs.zero_()
+        hist.zero_()
+        nxt = (x0 * c_in0).to(unet_in.dtype)
+        C = x0.shape[-1]
+        B = x0.shape[0]
+        unet_in[:B, ..., :C].copy_(nxt)
+        if cfg:
+            unet_in[B:, ..., :C].copy_(nxt)
+        return
+    ext().latent_init(x0.contiguous(), float(c_in0), x, xs, hist, unet_in, int(cfg))
+
+
+def finalize_latents(x: torch.Tensor, z: torch.Tensor, finite: torch.Tensor) -> None:
+    """z = bf16(x); finite[0] = 1 iff every element of x is finite (uint8 device flag)."""
+    if not _use_hip(x):
+        z.copy_(x.to(z.dtype))
+        finite.fill_(int(bool(torch.isfinite(x).all())))
+        return
+    ext().finalize_latents(x, z, finite)
 
 
 def latent_step(eps: torch.Tensor, x: torch.Tensor, hist: torch.Tensor, xs: torch.Tensor,

@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
+#include <hip/hip_ext.h>
 
 #include "kernels.h"
 
@@ -500,9 +501,65 @@ void to_uint8(const at::Tensor& x, at::Tensor& out) {
 }
 
 void timestep_embedding(const at::Tensor& t, at::Tensor& out, int64_t flip, double shift) {
-  CHECK_DEV(t);
-  launch_timestep_embedding(t.data_ptr<float>(), out.data_ptr<float>(), (int)t.size(0), (int)out.size(1), (int)flip,
-                            (float)shift, cur_stream());
+  CHECK_DEV(t); CHECK_CONTIG(t); CHECK_CONTIG(out);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) == t.numel() && out.size(1) % 2 == 0,
+              "timestep_embedding: t f32 [B], out [B, dim]");
+  const int bf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "timestep_embedding: out f32 or bf16");
+  launch_timestep_embedding(t.data_ptr<float>(), out.data_ptr(), (int)t.size(0), (int)out.size(1), (int)flip,
+                            (float)shift, bf, cur_stream());
+}
+
+void gather_add(const at::Tensor& table, const at::Tensor& ids, const c10::optional<at::Tensor>& pos, int64_t seq,
+                at::Tensor& out) {
+  CHECK_DEV(table); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(ids); CHECK_BF16(out); CHECK_CONTIG(out);
+  TORCH_CHECK(ids.scalar_type() == at::kInt && ids.is_cuda(), "gather_add: int32 device ids");
+  const int D = (int)table.size(-1);
+  const long long rows = ids.numel();
+  TORCH_CHECK(D % 8 == 0 && out.numel() == rows * D, "gather_add: D % 8 == 0, out [rows, D]");
+  const uint16_t* pp = opt_bptr(pos);
+  TORCH_CHECK(pp == nullptr || (seq > 0 && pos->size(-1) == D && pos->numel() >= seq * D), "gather_add: pos [>= seq, D]");
+  launch_gather_add(bptr(table), ids.data_ptr<int>(), pp, (int)(seq > 0 ? seq : 1), D, rows, bptr_mut(out),
+                    cur_stream());
+}
+
+void concat2(const at::Tensor& a, const at::Tensor& b, at::Tensor& out) {
+  CHECK_DEV(a); CHECK_BF16(a); CHECK_CONTIG(a); CHECK_DEV(b); CHECK_CONTIG(b); CHECK_BF16(out); CHECK_CONTIG(out);
+  const int Da = (int)a.size(-1), Db = (int)b.size(-1);
+  const long long rows = a.numel() / Da;
+  const int f32 = b.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || b.scalar_type() == at::kBFloat16, "concat2: b bf16 or f32");
+  TORCH_CHECK(Da % 8 == 0 && Db % 8 == 0 && b.numel() == rows * Db && out.numel() == rows * (Da + Db),
+              "concat2: [rows, Da] + [rows, Db] -> [rows, Da + Db], D % 8 == 0");
+  launch_concat2(bptr(a), Da, b.data_ptr(), Db, f32, rows, bptr_mut(out), cur_stream());
+}
+
+void silu_(at::Tensor& x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.numel() % 8 == 0, "silu_: numel % 8 == 0");
+  launch_silu_bf16(bptr_mut(x), x.numel(), cur_stream());
+}
+
+void latent_init(const at::Tensor& x0, double c_in0, at::Tensor& x, at::Tensor& xs, at::Tensor& hist, at::Tensor& unet_in,
+                 int64_t cfg) {
+  CHECK_DEV(x0); CHECK_CONTIG(x0); CHECK_CONTIG(x); CHECK_CONTIG(xs); CHECK_CONTIG(hist); CHECK_BF16(unet_in);
+  CHECK_CONTIG(unet_in);
+  TORCH_CHECK(x0.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat && xs.scalar_type() == at::kFloat &&
+              hist.scalar_type() == at::kFloat, "latent_init: f32 latents");
+  const long long n = x.numel();
+  const int cin = (int)x.size(-1), cstride = (int)unet_in.size(-1);
+  TORCH_CHECK(x0.numel() == n && xs.numel() == n && hist.numel() % n == 0 && cstride >= cin &&
+              unet_in.numel() == (cfg ? 2 : 1) * (n / cin) * cstride, "latent_init: shape mismatch");
+  launch_latent_init(x0.data_ptr<float>(), (float)c_in0, x.data_ptr<float>(), xs.data_ptr<float>(),
+                     hist.data_ptr<float>(), (int)(hist.numel() / n), bptr_mut(unet_in), n, (int)cfg, cin, cstride,
+                     cur_stream());
+}
+
+void finalize_latents(const at::Tensor& x, at::Tensor& z, at::Tensor& finite) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(z); CHECK_CONTIG(z);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && z.numel() == x.numel() && finite.scalar_type() == at::kByte &&
+              finite.numel() >= 1 && finite.is_cuda(), "finalize_latents: f32 x -> bf16 z, uint8 flag");
+  launch_finalize_latents(x.data_ptr<float>(), bptr_mut(z), x.numel(), finite.data_ptr<uint8_t>(), cur_stream());
 }
 
 void latent_step(const at::Tensor& eps, at::Tensor& x, at::Tensor& hist, at::Tensor& xs, const at::Tensor& coef,
@@ -533,6 +590,29 @@ void latent_step(const at::Tensor& eps, at::Tensor& x, at::Tensor& hist, at::Ten
                      h0 ? buf0->numel() * buf0->element_size() : 0, h1 ? tab1->data_ptr() : nullptr,
                      h1 ? buf1->data_ptr() : nullptr, h1 ? buf1->numel() * buf1->element_size() : 0, rows,
                      cur_stream());
+}
+
+// A HIP stream whose kernels may only run on the CUs of ``mask`` (bit i of word i / 32 = CU i):
+// the serving scorer gets a few CUs of its own and the generation stream the rest, so a guess is
+// never queued behind a wave of denoise workgroups (verdict r2 item 6).  Returned as the raw
+// handle for torch.cuda.ExternalStream; it lives for the process.
+int64_t cu_mask_stream(int64_t device, const std::vector<int64_t>& mask) {
+  TORCH_CHECK(!mask.empty(), "cu_mask_stream: empty mask");
+  std::vector<uint32_t> m(mask.begin(), mask.end());
+  int prev = 0;
+  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice");
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice");
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data());
+  (void)hipSetDevice(prev);
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask failed: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(s);
+}
+
+int64_t cu_count(int64_t device) {
+  hipDeviceProp_t p;
+  TORCH_CHECK(hipGetDeviceProperties(&p, (int)device) == hipSuccess, "hipGetDeviceProperties");
+  return p.multiProcessorCount;
 }
 
 void advance_step(at::Tensor& step) { launch_advance_step(step.data_ptr<int>(), cur_stream()); }
@@ -657,9 +737,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gaussian_blur", &gaussian_blur, nogil());
   m.def("to_uint8", &to_uint8, nogil());
   m.def("timestep_embedding", &timestep_embedding, nogil());
+  m.def("gather_add", &gather_add, nogil());
+  m.def("concat2", &concat2, nogil());
+  m.def("silu_", &silu_, nogil());
+  m.def("latent_init", &latent_init, nogil());
+  m.def("finalize_latents", &finalize_latents, nogil());
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());
+  m.def("cu_mask_stream", &cu_mask_stream);
+  m.def("cu_count", &cu_count);
   m.def("softmax_rows", &softmax_rows, nogil());
   m.def("rms_norm", &rms_norm, nogil());
   m.def("rope_kv", &rope_kv, nogil());

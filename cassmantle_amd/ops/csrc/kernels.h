@@ -154,7 +154,16 @@ void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, 
 void launch_gaussian_blur(const void* img, int u8, int H, int W, int C, const float* w, int R,
                           float* tmp, void* out, hipStream_t s);
 void launch_to_uint8(const uint16_t* x, uint8_t* out, long long n, hipStream_t s);
-void launch_timestep_embedding(const float* t, float* out, int B, int dim, int flip, float shift, hipStream_t s);
+void launch_timestep_embedding(const float* t, void* out, int B, int dim, int flip, float shift, int out_bf16,
+                               hipStream_t s);
+void launch_gather_add(const uint16_t* table, const int* ids, const uint16_t* pos, int seq, int D, long long rows,
+                       uint16_t* out, hipStream_t s);
+void launch_concat2(const uint16_t* a, int Da, const void* b, int Db, int b_f32, long long rows, uint16_t* out,
+                    hipStream_t s);
+void launch_silu_bf16(uint16_t* x, long long n, hipStream_t s);
+void launch_latent_init(const float* x0, float c_in0, float* x, float* xs, float* hist, int nhist, uint16_t* unet_in,
+                        long long n, int cfg, int cin, int cstride, hipStream_t s);
+void launch_finalize_latents(const float* x, uint16_t* z, long long n, uint8_t* finite, hipStream_t s);
 // CFG combine + scheduler update + next UNet input (channel-padded to cstride); the optional
 // tables' rows for step+1 (time conditioning) are copied into buf0/buf1 by extra blocks
 void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef, const int* step,

@@ -62,20 +62,31 @@ class _StepState:
                  cfg: bool, added: Optional[dict]):
         self.B, self.cfg = B, cfg
         nb = 2 * B if cfg else B
-        self.x = torch.zeros((B, h, w, 4), device=device, dtype=torch.float32)
-        self.xs = torch.zeros_like(self.x)
-        self.hist = torch.zeros((4, B, h, w, 4), device=device, dtype=torch.float32)
+        # (latent_init fills x / xs / hist at every load; zero fills on the GPU are HIP kernels)
+        self.x = torch.empty((B, h, w, 4), device=device, dtype=torch.float32)
+        self.xs = torch.empty_like(self.x)
+        self.hist = torch.empty((4, B, h, w, 4), device=device, dtype=torch.float32)
         # on the GPU the UNet input carries 4 zero channels: conv_in then reads whole 16-byte
         # k-chunks with no per-step pad copy (the latent-step kernel writes channels 0..3)
-        self.unet_in = torch.zeros((nb, h, w, 8 if torch.device(device).type == "cuda" else 4), device=device,
-                                   dtype=dtype)
-        self.ctx = torch.zeros_like(ctx)
+        self.unet_in = ops.zero_(torch.empty((nb, h, w, 8 if torch.device(device).type == "cuda" else 4),
+                                             device=device, dtype=dtype))
+        self.ctx = torch.empty_like(ctx)
         self.coef = torch.from_numpy(plan.table).to(device)
         self.tsteps = torch.from_numpy(plan.table[:, 14].copy()).to(device)
-        self.step = torch.zeros((1,), device=device, dtype=torch.int32)
+        # the time table's per-row inputs, built on the host once per state: t of row e*nb + b
+        # and the row -> image index of the add-embedding repeat (no device repeat kernels)
+        E = plan.table.shape[0]
+        self.t_rep = torch.from_numpy(np.repeat(plan.table[:, 14].astype(np.float32), nb)).to(device)
+        self.rep_ids = torch.from_numpy((np.arange(E * nb) % nb).astype(np.int32)).to(device)
+        self.tid_rep = None
+        if added is not None:
+            self.tid_rep = added["time_ids"].detach().cpu().repeat(E, 1).to(device)
+        self.z = torch.empty((B, h, w, 4), device=device, dtype=dtype)      # bf16 latents for the VAE
+        self.finite = torch.empty((16,), device=device, dtype=torch.uint8)[:1]   # set by finalize_latents
+        self.step = ops.zero_(torch.empty((4,), device=device, dtype=torch.int32))[:1]
         self.added = None
         if added is not None:
-            self.added = {k: torch.zeros_like(v) for k, v in added.items()}
+            self.added = {k: torch.empty_like(v) for k, v in added.items()}
         self.graph: Optional["torch.cuda.CUDAGraph"] = None
         self.plan = plan
         # per-plan time conditioning (UNet.time_table), refilled in place every generation
@@ -94,17 +105,9 @@ class _StepState:
             self.tb_tab.copy_(tb)
 
     def load(self, x0: torch.Tensor, ctx: torch.Tensor, added: Optional[dict]):
-        self.x.copy_(x0)
-        ops.zero_(self.xs)
-        ops.zero_(self.hist)
+        # x, xs, hist and the first UNet input (both CFG halves) in one kernel
+        ops.latent_init(x0, self.plan.c_in0, self.x, self.xs, self.hist, self.unet_in, self.cfg)
         self.ctx.copy_(ctx)
-        nxt = (x0 * self.plan.c_in0).to(self.unet_in.dtype)
-        C = x0.shape[-1]
-        if self.cfg:
-            self.unet_in[: self.B, ..., :C].copy_(nxt)
-            self.unet_in[self.B:, ..., :C].copy_(nxt)
-        else:
-            self.unet_in[..., :C].copy_(nxt)
         if self.temb_tab is not None:
             self.temb_cur.copy_(self.temb_tab[0])
             self.tb_cur.copy_(self.tb_tab[0])
@@ -116,7 +119,8 @@ class _StepState:
 
 class StableDiffusion:
     def __init__(self, spec: PipelineSpec, device=None, dtype=torch.bfloat16, seed: int = 0,
-                 use_graphs: bool = True, fp8_attention: bool = False, overlap_decode: bool = False) -> None:
+                 use_graphs: bool = True, fp8_attention: bool = False, overlap_decode: bool = False,
+                 stream: Optional["torch.cuda.Stream"] = None) -> None:
         self.spec = spec
         self.device = torch.device(device) if device is not None else default_device()
         self.dtype = dtype
@@ -124,13 +128,19 @@ class StableDiffusion:
         self.fp8 = fp8_attention
         self.text_encoders = [CLIPTextEncoder(c, seed=seed + i, dtype=dtype).to(self.device).eval()
                               for i, c in enumerate(spec.text)]
-        self.unet = UNet(spec.unet, seed=seed, dtype=dtype).to(self.device).eval()
-        self.vae = VAEDecoder(spec.vae, seed=seed, dtype=dtype).to(self.device).eval()
+        # derived weights (fused projections, LayerNorm folds, parity-folded upsampling convs,
+        # padded conv_in, scaled post-quant conv) are computed on the CPU BEFORE the move: no
+        # setup kernel of ATen / hipBLASLt / rocBLAS runs on the GPU (verdict r2 item 7)
+        self.unet = UNet(spec.unet, seed=seed, dtype=dtype).prepare().to(self.device).eval()
+        self.vae = VAEDecoder(spec.vae, seed=seed, dtype=dtype).prepare().to(self.device).eval()
         self._states: Dict[tuple, _StepState] = {}
         self.timings: Dict[str, float] = {}
         # generation runs on its own stream (never the legacy default stream), so a serving
         # process can overlap it with the scorer's high-priority stream (BASELINE config 5)
-        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # (``stream``: a caller-made stream, e.g. CU-masked by runtime.cumask so the serving
+        # scorer keeps a few CUs of its own)
+        self.stream = stream if stream is not None else (
+            torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None)
         # stage overlap (opt-in): the VAE decode of generation i runs on its own stream,
         # concurrently with the encode + denoise of generation i+1 (the latents it reads are a
         # bf16 copy, so the next denoise may overwrite the step state at once).  Measured OFF by
@@ -166,7 +176,7 @@ class StableDiffusion:
             hs.append(h)
             if p is not None:
                 pooled = p
-        ctx = torch.cat(hs, dim=-1)
+        ctx = ops.concat_last(hs[0], hs[1]) if len(hs) == 2 else torch.cat(hs, dim=-1)
         R = self.spec.resolution
         tid = torch.tensor([R, R, 0, 0, R, R], device=self.device, dtype=torch.float32).repeat(len(texts), 1)
         return ctx, {"time_ids": tid, "text_embeds": pooled}
@@ -179,6 +189,11 @@ class StableDiffusion:
         ops.latent_step(eps, st.x, st.hist, st.xs, st.coef, st.step, st.unet_in, st.cfg,
                         rows=[(st.temb_tab, st.temb_cur), (st.tb_tab, st.tb_cur)])
         ops.advance_step(st.step)
+
+    def prepare(self) -> None:
+        """Recompute the derived weights (after an in-place weight load)."""
+        self.unet.prepare()
+        self.vae.prepare()
 
     def _state(self, B: int, ctx: torch.Tensor, plan: SchedulePlan, added) -> _StepState:
         key = (B, self.latent_size, plan.name, plan.evals, float(plan.table[0, 13]), tuple(ctx.shape))
@@ -210,12 +225,15 @@ class StableDiffusion:
                 added: Optional[dict] = None) -> torch.Tensor:
         B = latents.shape[0]
         st = self._state(B, ctx, plan, added)
+        self._last_state = st
         # cross-attention K/V of the (loop-invariant) text context: one GEMM per generation,
         # written into per-shape buffers that the captured step graph reads
         self.unet.set_context(ctx, fp8=self.fp8)
         # time embedding + every ResNet's time bias for all timesteps of the plan: one batched
         # MLP + GEMM per generation (in place, so a captured step graph reads the new values)
-        st.load_time(*self.unet.time_table(st.tsteps, st.unet_in.shape[0], added))
+        added_t = dict(added, time_ids_rep=st.tid_rep) if added is not None and st.tid_rep is not None else added
+        st.load_time(*self.unet.time_table(st.tsteps, st.unet_in.shape[0], added_t, t_rep=st.t_rep,
+                                           rep_ids=st.rep_ids))
         if self.use_graphs and st.graph is None:
             st.load(latents, ctx, added)
             self._capture(st)
@@ -268,8 +286,13 @@ class StableDiffusion:
                 x0 = self.init_latents(seeds, plan)
             with span("denoise", self.stream):
                 x = self.denoise(ctx, x0, plan, added)
-            self.last_finite = torch.isfinite(x).all()
-            z = x.to(self.dtype)
+            # bf16 latents for the VAE + finiteness flag of the fp32 latents, one kernel (the
+            # flag is checked before the uint8 decode, where NaN/Inf would silently become a
+            # garbage image)
+            st = self._last_state
+            z = st.z if st.z.shape == x.shape else torch.empty(x.shape, device=x.device, dtype=self.dtype)
+            ops.finalize_latents(x, z, st.finite)
+            self.last_finite = st.finite
             self.last_latents = z
             if self.decode_stream is None:
                 with span("decode", self.stream):
@@ -298,12 +321,12 @@ class StableDiffusion:
                 with torch.cuda.stream(out):
                     host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
                     host.copy_(img, non_blocking=True)
-                    ok = torch.empty((), dtype=torch.bool, pin_memory=True)
+                    ok = torch.empty(finite.shape, dtype=finite.dtype, pin_memory=True)
                     ok.copy_(finite, non_blocking=True)
                 out.synchronize()
-                arr, fin = host.numpy(), bool(ok)
+                arr, fin = host.numpy(), bool(ok.reshape(-1)[0])
             else:
-                arr, fin = img.numpy(), bool(finite)
+                arr, fin = img.numpy(), bool(finite.reshape(-1)[0])
             if not fin:
                 raise ImageGenerationError("non-finite latents (NaN/Inf in the denoise loop)")
         return [arr[i].copy() for i in range(arr.shape[0])]
@@ -323,9 +346,9 @@ class DiffusionImageGenerator(ImageGenerator):
     def __init__(self, model: str = "sd15", device=None, steps: Optional[int] = None,
                  guidance: Optional[float] = None, scheduler: Optional[str] = None,
                  use_graphs: bool = True, fp8_attention: bool = False, seed: int = 0,
-                 dtype=torch.bfloat16, weights_path: Optional[str] = None) -> None:
+                 dtype=torch.bfloat16, weights_path: Optional[str] = None, stream=None) -> None:
         self.sd = StableDiffusion(SPECS[model], device=device, use_graphs=use_graphs,
-                                  fp8_attention=fp8_attention, seed=seed, dtype=dtype)
+                                  fp8_attention=fp8_attention, seed=seed, dtype=dtype, stream=stream)
         self.weights_loaded: Optional[Dict[str, int]] = None
         if weights_path:
             # diffusers-layout checkpoint (ModelConfig.weights_path); random init otherwise

@@ -32,6 +32,22 @@ def model_dtype(cfg: Config, device: str) -> torch.dtype:
     return dt
 
 
+_STREAMS: dict = {}
+
+
+def reserved_streams(cfg: Config, device: str):
+    """(scorer stream, generation stream) with ``scorer_reserved_cus`` CUs for the scorer, one
+    pair per device and process; (None, None) when no reservation is configured."""
+    n = cfg.model.scorer_reserved_cus
+    if n <= 0 or not str(device).startswith("cuda"):
+        return None, None
+    key = (str(device), n)
+    if key not in _STREAMS:
+        from .cumask import reserved_streams as _rs
+        _STREAMS[key] = _rs(device, n)
+    return _STREAMS[key]
+
+
 def build_scorer(cfg: Config, device: Optional[str] = None, wrap=None):
     """MiniLM-encoder (or word-vector) backend behind the micro-batching scorer.  ``wrap`` maps
     the local backend to the one the scorer calls (multi-GPU: ``parallel.scoring.ShardedSimilarity``)."""
@@ -43,7 +59,7 @@ def build_scorer(cfg: Config, device: Optional[str] = None, wrap=None):
         from ..scoring.encoder import EncoderBackend
         # high-priority stream: guess scoring is dispatched ahead of queued denoise kernels
         backend = EncoderBackend(device=dev, stream_priority=-1 if dev.startswith("cuda") else None,
-                                 dtype=model_dtype(cfg, dev))
+                                 dtype=model_dtype(cfg, dev), stream=reserved_streams(cfg, dev)[0])
         if cfg.model.scorer_weights:
             from ..models.weights import load_bert, read_safetensors
             missing = load_bert(backend.model, read_safetensors(cfg.model.scorer_weights))
@@ -111,7 +127,8 @@ def build_image_generator(cfg: Config, device: Optional[str] = None) -> ImageGen
     return DiffusionImageGenerator(m.image_model, device=dev, steps=m.steps,
                                    guidance=m.guidance_scale, scheduler=m.scheduler,
                                    use_graphs=m.use_graphs, fp8_attention=m.fp8_attention, seed=m.seed,
-                                   dtype=model_dtype(cfg, dev), weights_path=m.weights_path)
+                                   dtype=model_dtype(cfg, dev), weights_path=m.weights_path,
+                                   stream=reserved_streams(cfg, dev)[1])
 
 
 def build_service(cfg: Config, image_gen_for_room: Optional[Callable[[str], ImageGenerator]] = None,

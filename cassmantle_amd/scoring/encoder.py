@@ -34,10 +34,10 @@ class EncoderBackend(SimilarityBackend):
 
     def __init__(self, cfg: BertConfig = MINILM_L6, device: str = "cpu", seed: int = 0,
                  max_len: int = 16, dtype=torch.bfloat16, stream_priority: Optional[int] = None,
-                 use_graphs: bool = True) -> None:
+                 use_graphs: bool = True, stream=None) -> None:
         self.device = torch.device(device)
-        self.stream = None
-        if self.device.type == "cuda":
+        self.stream = stream                      # e.g. a CU-masked stream (runtime.cumask)
+        if self.device.type == "cuda" and self.stream is None:
             self.stream = torch.cuda.Stream(device=self.device, priority=stream_priority or 0)
         self.model = MiniLMEncoder(cfg, seed=seed, dtype=dtype, max_len=max_len).to(self.device).eval()
         self.max_len = max_len

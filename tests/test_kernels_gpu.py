@@ -718,3 +718,100 @@ def test_ln_gemm_bitwise_stable_under_concurrency():
     torch.cuda.synchronize()
     bad = sum(int(not torch.equal(y, ref_out)) for y in outs)
     assert bad == 0, f"{bad}/30 concurrent runs differ from the quiet result"
+
+
+# ---------------------------------------------------------------- generation glue (round 3)
+def test_gather_add_embedding_and_row_gather():
+    table = rnd(1000, 64, seed=11)
+    pos = rnd(77, 64, scale=0.1, seed=12)
+    ids = torch.randint(0, 1000, (3, 77), generator=torch.Generator().manual_seed(1)).to(DEV)
+    got = ops.gather_add(table, ids.int(), pos)
+    exp = table[ids.long()] + pos[None]                    # bf16 add, as the eager model
+    assert torch.equal(got, exp)
+    rows = torch.tensor([5, 0, 999, 5], dtype=torch.int32, device=DEV)
+    assert torch.equal(ops.gather_add(table, rows), table[rows.long()])
+
+
+@pytest.mark.parametrize("bdtype", [torch.bfloat16, torch.float32])
+def test_concat_last(bdtype):
+    a = rnd(6, 1280, seed=13)
+    b = rnd(6, 1536, seed=14, dtype=bdtype)
+    got = ops.concat_last(a, b)
+    assert torch.equal(got, torch.cat([a, b.to(torch.bfloat16)], dim=-1))
+
+
+def test_silu_inplace():
+    x = rnd(12, 1280, scale=3.0, seed=15)
+    exp = torch.nn.functional.silu(x.float())
+    ops.silu_(x)
+    assert rel_err(x, exp) < 1e-2
+
+
+def test_timestep_embedding_bf16_out():
+    t = torch.tensor([1.0, 500.0, 981.0], device=DEV)
+    a = ops.timestep_embedding(t, 320)
+    b = ops.timestep_embedding(t, 320, out_dtype=torch.bfloat16)
+    assert b.dtype == torch.bfloat16 and torch.equal(b, a.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("cfg", [True, False])
+def test_latent_init_matches_reference(cfg):
+    B, h, C8 = 2, 8, 8
+    nb = 2 * B if cfg else B
+    x0 = torch.randn(B, h, h, 4, generator=torch.Generator().manual_seed(3)).to(DEV)
+    outs = []
+    for mode in ("hip", "torch"):
+        x = torch.full((B, h, h, 4), 7.0, device=DEV)
+        xs = torch.full_like(x, 7.0)
+        hist = torch.full((4, B, h, h, 4), 7.0, device=DEV)
+        u = torch.zeros((nb, h, h, C8), device=DEV, dtype=torch.bfloat16)
+        if mode == "hip":
+            ops.latent_init(x0, 0.5, x, xs, hist, u, cfg)
+        else:
+            x.copy_(x0); xs.zero_(); hist.zero_()
+            for k in range(2 if cfg else 1):
+                u[k * B:(k + 1) * B, ..., :4] = (x0 * 0.5).to(torch.bfloat16)
+        outs.append((x, xs, hist, u))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_finalize_latents_flag():
+    x = torch.randn(2, 16, 16, 4, device=DEV)
+    z = torch.empty_like(x, dtype=torch.bfloat16)
+    f = torch.empty((1,), device=DEV, dtype=torch.uint8)
+    ops.finalize_latents(x, z, f)
+    assert torch.equal(z, x.to(torch.bfloat16)) and int(f.item()) == 1
+    x[1, 7, 3, 2] = float("nan")
+    ops.finalize_latents(x, z, f)
+    assert int(f.item()) == 0
+    x[1, 7, 3, 2] = float("inf")
+    ops.finalize_latents(x, z, f)
+    assert int(f.item()) == 0
+
+
+def test_cu_masked_streams_run_kernels():
+    """the scorer / generation CU reservation (runtime/cumask.py): both masked streams run HIP
+    kernels correctly, and a captured graph replays on the masked generation stream"""
+    from cassmantle_amd.runtime.cumask import reserved_streams, split_cus
+    mine, rest = split_cus(256, 8)
+    assert len(mine) == 8 and len(rest) == 248 and not set(mine) & set(rest)
+    s_score, s_gen = reserved_streams(DEV, 8)
+    x = rnd(512, 640, seed=16)
+    w = rnd(640, 640, scale=640 ** -0.5, seed=17)
+    exp = ops.linear(x, w)
+    torch.cuda.synchronize()
+    for s in (s_score, s_gen):
+        with torch.cuda.stream(s):
+            y = ops.linear(x, w)
+        s.synchronize()
+        assert torch.equal(y, exp)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s_gen):
+        ops.linear(x, w)
+        s_gen.synchronize()
+        with torch.cuda.graph(g, stream=s_gen):
+            y = ops.linear(x, w)
+        g.replay()
+    s_gen.synchronize()
+    assert torch.equal(y, exp)

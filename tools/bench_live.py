@@ -50,6 +50,8 @@ def parse():
                          "on the legacy default stream it queued behind whole generations, "
                          "pipeline.StableDiffusion.generate_tensor docstring)")
     ap.add_argument("--window-ms", type=float, default=1.0)
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="CUs reserved for the scorer (CU-masked streams, runtime/cumask.py); 0 = none")
     ap.add_argument("--score-topology", choices=("central", "sharded"), default="central",
                     help="as serve.py's GameConfig.score_topology: rank-0 scoring, or micro-batches of "
                          ">= --shard-min pairs split over every rank (C1 broadcast + C3 gather, parallel/scoring.py)")
@@ -89,8 +91,12 @@ def main():
     ctx = cdist.init_from_env()
     rank, world, dev = ctx.rank, ctx.world_size, ctx.device
     n_players = a.players if rank == 0 else 0          # rank-0-central scoring, as serve.py
-    sd = StableDiffusion(SPECS[a.model], device=dev, seed=0)
-    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
+    s_score = s_gen = None
+    if a.reserve_cus > 0:
+        from cassmantle_amd.runtime.cumask import reserved_streams
+        s_score, s_gen = reserved_streams(dev, a.reserve_cus)
+    sd = StableDiffusion(SPECS[a.model], device=dev, seed=0, stream=s_gen)
+    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority, stream=s_score)
     sharded = follower = None
     if a.score_topology == "sharded" and world > 1:
         from cassmantle_amd.parallel.scoring import ShardedSimilarity, new_scoring_group
@@ -168,7 +174,7 @@ def main():
             "think_ms": a.think_ms, "idle_p50_ms": round(s[1], 3), "idle_p99_ms": round(s[2], 3),
             "load_p50_ms": round(s[3], 3), "load_p99_ms": round(s[4], 3), "requests": int(s[5]),
             "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
-            "score_topology": a.score_topology,
+            "score_topology": a.score_topology, "reserved_cus": a.reserve_cus,
             "sharded_pairs": sharded.sharded_pairs if sharded is not None else 0,
             "config": {"model": a.model, "batch_per_room": a.batch, "graphs": bool(sd.use_graphs)}}), flush=True)
     cdist.shutdown()

@@ -14,8 +14,14 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--per", type=float, default=1.0)
+    ap.add_argument("--skip-before", default=None,
+                    help="ignore kernels before the first one whose name contains this string")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if a.skip_before:
+        first = next((i for i, r in enumerate(rows) if a.skip_before in r["Kernel_Name"]), 0)
+        rows = rows[first:]
     by_grid = collections.defaultdict(lambda: [0, 0.0])
     fam = collections.defaultdict(float)
     for r in rows:
@@ -31,6 +37,13 @@ def main():
         print(f"  {v / 1e3 / a.per:8.3f} ms {100 * v / tot:5.1f}%  {k}")
     for k, v in sorted(by_grid.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{v[1] / 1e3 / a.per:8.3f}ms {100 * v[1] / tot:5.1f}% n={v[0]:5d} avg={v[1] / v[0]:8.1f}us {k}")
+    # kernels that are not this repository's (in-tree kernels live in an anonymous namespace of
+    # cassmantle_amd/ops/csrc): ATen, hipBLASLt (Cijk_*), rocBLAS, HIP runtime blits
+    ours = [r for r in rows if "anonymous namespace" in r["Kernel_Name"] or r["Kernel_Name"].startswith(("attn_", "gemm_"))]
+    other = collections.Counter(r["Kernel_Name"][:90] for r in rows if r not in ours)
+    print(f"non-in-tree kernels: {sum(other.values())} launches of {len(other)} kinds")
+    for k, n in other.most_common(30):
+        print(f"  {n:6d}  {k}")
 
 
 if __name__ == "__main__":
