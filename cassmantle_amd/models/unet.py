@@ -325,13 +325,12 @@ class UNet(nn.Module):
                 m._kv = None
                 m._kv8 = None
             return
-        kv = ops.linear(ctx, self._kv_w)                            # [B, L, sum 2C]
-        key = tuple(kv.shape)
+        key = (*ctx.shape[:-1], self._kv_w.shape[0])               # [B, L, sum 2C]
         buf = self._kv_bufs.get(key)
-        if buf is None:
-            self._kv_bufs[key] = buf = kv
+        if buf is None or buf.device != ctx.device:
+            self._kv_bufs[key] = buf = ops.linear(ctx, self._kv_w)
         else:
-            buf.copy_(kv)
+            ops.linear(ctx, self._kv_w, out=buf)                     # refilled in place
         for m in ca:
             m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
             if fp8 and m.head_dim == 64 and ops._use_hip(buf):

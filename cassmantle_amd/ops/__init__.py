@@ -135,8 +135,9 @@ def channel_stats(y: torch.Tensor, stats: torch.Tensor) -> None:
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: Optional[str] = None,
-           stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+           stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu).
+    ``out``: a contiguous [..., N] buffer of x's dtype to write y into (else a new tensor).
 
     ``stats`` (:func:`new_stats` [B, N, 2], zeroed; B = x.shape[0]): per-(image, channel) sum and
     sum-of-squares of y are accumulated into it by the GEMM epilogue, for a following
@@ -148,17 +149,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             y = ref.linear(x, w, bias, residual, act)
         if stats is not None:
             channel_stats_ref(y, stats)
-        return y
+        return y if out is None else out.copy_(y)
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
     N = w.shape[0] // 2 if act in ("geglu", "swiglu") else w.shape[0]
-    out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
+    if out is None:
+        out = torch.empty((x2.shape[0], N), device=x.device, dtype=x.dtype)
+    else:
+        assert out.is_contiguous() and out.dtype == x.dtype and out.numel() == x2.shape[0] * N, "linear: bad out"
+    o2 = out.view(x2.shape[0], N)
     r2 = residual.reshape(-1, N) if residual is not None else None
     hw = x2.shape[0] // x.shape[0] if stats is not None else 0
-    _launch(ext().gemm, x2, w, bias, r2, out, _ACT[act], stats, hw)
-    return out.reshape(*x.shape[:-1], N)
+    _launch(ext().gemm, x2, w, bias, r2, o2, _ACT[act], stats, hw)
+    return out.view(*x.shape[:-1], N)
 
 
 def ln_fold(ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], w: torch.Tensor,
@@ -690,6 +695,16 @@ def latent_step(eps: torch.Tensor, x: torch.Tensor, hist: torch.Tensor, xs: torc
         return
     (t0, b0), (t1, b1) = (rows + [(None, None), (None, None)])[:2]
     ext().latent_step(eps, x, hist, xs, coef, step, unet_in, int(cfg), t0, b0, t1, b1)
+
+
+def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """``dst.copy_(src)`` for same-dtype same-size contiguous device tensors as an in-tree kernel
+    (16-byte accesses; no runtime blit node in a generation's trace); anything else -> torch."""
+    if (not _use_hip(dst) or src.device != dst.device or src.dtype != dst.dtype or src.numel() != dst.numel()
+            or not src.is_contiguous() or not dst.is_contiguous() or src.data_ptr() % 16 or dst.data_ptr() % 16):
+        return dst.copy_(src)
+    ext().dcopy(src, dst)
+    return dst
 
 
 def zero_(t: torch.Tensor) -> torch.Tensor:

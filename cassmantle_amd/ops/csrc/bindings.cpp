@@ -555,10 +555,20 @@ void latent_init(const at::Tensor& x0, double c_in0, at::Tensor& x, at::Tensor& 
                      cur_stream());
 }
 
+void dcopy(const at::Tensor& src, at::Tensor& dst) {
+  CHECK_DEV(src); CHECK_CONTIG(src); CHECK_DEV(dst); CHECK_CONTIG(dst);
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type() && src.numel() == dst.numel(), "dcopy: same dtype and size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "dcopy: 16-byte aligned");
+  launch_copy(src.data_ptr(), dst.data_ptr(), (long long)src.numel() * src.element_size(), cur_stream());
+}
+
 void finalize_latents(const at::Tensor& x, at::Tensor& z, at::Tensor& finite) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(z); CHECK_CONTIG(z);
   TORCH_CHECK(x.scalar_type() == at::kFloat && z.numel() == x.numel() && finite.scalar_type() == at::kByte &&
               finite.numel() >= 1 && finite.is_cuda(), "finalize_latents: f32 x -> bf16 z, uint8 flag");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(z.data_ptr()) % 8 == 0,
+              "finalize_latents: x 16-byte / z 8-byte aligned");
   launch_finalize_latents(x.data_ptr<float>(), bptr_mut(z), x.numel(), finite.data_ptr<uint8_t>(), cur_stream());
 }
 
@@ -742,6 +752,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_", &silu_, nogil());
   m.def("latent_init", &latent_init, nogil());
   m.def("finalize_latents", &finalize_latents, nogil());
+  m.def("dcopy", &dcopy, nogil());
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());

@@ -163,6 +163,7 @@ void launch_concat2(const uint16_t* a, int Da, const void* b, int Db, int b_f32,
 void launch_silu_bf16(uint16_t* x, long long n, hipStream_t s);
 void launch_latent_init(const float* x0, float c_in0, float* x, float* xs, float* hist, int nhist, uint16_t* unet_in,
                         long long n, int cfg, int cin, int cstride, hipStream_t s);
+void launch_copy(const void* src, void* dst, long long bytes, hipStream_t s);
 void launch_finalize_latents(const float* x, uint16_t* z, long long n, uint8_t* finite, hipStream_t s);
 // CFG combine + scheduler update + next UNet input (channel-padded to cstride); the optional
 // tables' rows for step+1 (time conditioning) are copied into buf0/buf1 by extra blocks

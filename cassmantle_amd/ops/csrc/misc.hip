@@ -301,17 +301,23 @@ __global__ void latent_init_kernel(const float* __restrict__ x0, float c_in0, fl
 }
 
 // end of the denoise loop: bf16 copy of the fp32 latents for the VAE, and a device flag that
-// stays 1 only if every latent is finite (the caller sets it to 1 first)
-__global__ void finalize_latents_kernel(const float* __restrict__ x, uint16_t* __restrict__ z, long long n,
-                                        uint8_t* __restrict__ finite) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  bool bad = false;
-  if (i < n) {
-    const float v = x[i];
-    z[i] = f2bf(v);
-    bad = !isfinite(v);
+// is 1 iff every latent is finite.  ONE block (the latents are 64-256K floats: a few us on one
+// CU) so the flag is written once, from the block-wide vote -- no memset node before it
+__global__ void __launch_bounds__(1024) finalize_latents_kernel(const float* __restrict__ x, uint16_t* __restrict__ z,
+                                                                long long n, uint8_t* __restrict__ finite) {
+  int bad = 0;
+  const long long n4 = n / 4;
+  for (long long i = threadIdx.x; i < n4; i += blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<uint2*>(z)[i] = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
+    bad |= !isfinite(v.x) | !isfinite(v.y) | !isfinite(v.z) | !isfinite(v.w);
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) finite[0] = 0;
+  for (long long i = 4 * n4 + threadIdx.x; i < n; i += blockDim.x) {
+    z[i] = f2bf(x[i]);
+    bad |= !isfinite(x[i]);
+  }
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) finite[0] = bad ? 0 : 1;
 }
 
 // zero-fill with 16-byte vector stores (the GroupNorm statistics slab cleared at the start of
@@ -320,6 +326,15 @@ __global__ void zero_kernel(uint4* __restrict__ p, long long n16, uint8_t* __res
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) p[i] = make_uint4(0, 0, 0, 0);
   if (i < ntail) tail[i] = 0;
+}
+
+// device-to-device copy with 16-byte vector accesses (the per-generation refills of a captured
+// step's input buffers: text context, time-table rows, add-embeds; was a runtime blit kernel)
+__global__ void copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, long long n16,
+                              const uint8_t* __restrict__ stail, uint8_t* __restrict__ dtail, int ntail) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+  if (i < ntail) dtail[i] = stail[i];
 }
 
 // row softmax with optional causal / key-length mask (S fp32 [rows][cols] -> P bf16)
@@ -510,8 +525,7 @@ void launch_latent_init(const float* x0, float c_in0, float* x, float* xs, float
 }
 
 void launch_finalize_latents(const float* x, uint16_t* z, long long n, uint8_t* finite, hipStream_t s) {
-  (void)hipMemsetAsync(finite, 1, 1, s);
-  hipLaunchKernelGGL(finalize_latents_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, x, z, n, finite);
+  hipLaunchKernelGGL(finalize_latents_kernel, dim3(1), dim3(1024), 0, s, x, z, n, finite);
 }
 
 void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, const float* coef, const int* step,
@@ -538,6 +552,16 @@ void launch_zero(void* p, long long bytes, hipStream_t s) {
   const unsigned blocks = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(p), n16,
                      reinterpret_cast<uint8_t*>(p) + n16 * 16, ntail);
+}
+
+void launch_copy(const void* src, void* dst, long long bytes, hipStream_t s) {
+  const long long n16 = bytes / 16;
+  const int ntail = (int)(bytes - n16 * 16);
+  const long long n = n16 > ntail ? n16 : ntail;
+  if (n == 0) return;
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16,
+                     reinterpret_cast<const uint8_t*>(src) + n16 * 16, reinterpret_cast<uint8_t*>(dst) + n16 * 16, ntail);
 }
 
 void launch_advance_step(int* step, hipStream_t s) {

@@ -88,6 +88,9 @@ class _StepState:
         if added is not None:
             self.added = {k: torch.empty_like(v) for k, v in added.items()}
         self.graph: Optional["torch.cuda.CUDAGraph"] = None
+        # captured VAE decode of ``z`` and its static uint8 output (StableDiffusion._decode)
+        self.vae_graph: Optional["torch.cuda.CUDAGraph"] = None
+        self.vae_img: Optional[torch.Tensor] = None
         self.plan = plan
         # per-plan time conditioning (UNet.time_table), refilled in place every generation
         self.temb_tab: Optional[torch.Tensor] = None
@@ -101,19 +104,20 @@ class _StepState:
             self.temb_tab, self.tb_tab = temb.clone(), tb.clone()
             self.temb_cur, self.tb_cur = temb[0].clone(), tb[0].clone()
         else:
-            self.temb_tab.copy_(temb)
-            self.tb_tab.copy_(tb)
+            ops.copy_(self.temb_tab, temb)
+            ops.copy_(self.tb_tab, tb)
 
     def load(self, x0: torch.Tensor, ctx: torch.Tensor, added: Optional[dict]):
         # x, xs, hist and the first UNet input (both CFG halves) in one kernel
         ops.latent_init(x0, self.plan.c_in0, self.x, self.xs, self.hist, self.unet_in, self.cfg)
-        self.ctx.copy_(ctx)
+        # (in-tree copy kernels: no runtime blit in a generation's trace)
+        ops.copy_(self.ctx, ctx)
         if self.temb_tab is not None:
-            self.temb_cur.copy_(self.temb_tab[0])
-            self.tb_cur.copy_(self.tb_tab[0])
+            ops.copy_(self.temb_cur, self.temb_tab[0])
+            ops.copy_(self.tb_cur, self.tb_tab[0])
         if added is not None:
             for k, v in added.items():
-                self.added[k].copy_(v)
+                ops.copy_(self.added[k], v)
         ops.zero_(self.step)
 
 
@@ -178,7 +182,7 @@ class StableDiffusion:
                 pooled = p
         ctx = ops.concat_last(hs[0], hs[1]) if len(hs) == 2 else torch.cat(hs, dim=-1)
         R = self.spec.resolution
-        tid = torch.tensor([R, R, 0, 0, R, R], device=self.device, dtype=torch.float32).repeat(len(texts), 1)
+        tid = torch.tensor([R, R, 0, 0, R, R], dtype=torch.float32).repeat(len(texts), 1).to(self.device)
         return ctx, {"time_ids": tid, "text_embeds": pooled}
 
     # ------------------------------------------------------------------ denoise
@@ -191,9 +195,13 @@ class StableDiffusion:
         ops.advance_step(st.step)
 
     def prepare(self) -> None:
-        """Recompute the derived weights (after an in-place weight load)."""
-        self.unet.prepare()
-        self.vae.prepare()
+        """Recompute the derived weights (after an in-place weight load).  Captured step / decode
+        graphs point at the old derived buffers, so the per-shape states are dropped (recaptured
+        on the next generation)."""
+        with self._lock:
+            self.unet.prepare()
+            self.vae.prepare()
+            self._states.clear()
 
     def _state(self, B: int, ctx: torch.Tensor, plan: SchedulePlan, added) -> _StepState:
         key = (B, self.latent_size, plan.name, plan.evals, float(plan.table[0, 13]), tuple(ctx.shape))
@@ -219,6 +227,28 @@ class StableDiffusion:
         with TRACER.capturing(), torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._unet_step(st)
         st.graph = g
+
+    def _decode(self, st: _StepState, z: torch.Tensor) -> torch.Tensor:
+        """VAE decode -> uint8 image.  With graphs, the decode of the state's latent buffer is
+        captured once per state and replayed (~200 eager launches per generation otherwise: host
+        time that also holds the GIL against a serving process's scorer thread); the replay's
+        static output is copied out, so the returned image outlives the next generation."""
+        if not self.use_graphs or z is not st.z:
+            return self.vae.decode_uint8(z)
+        if st.vae_graph is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self.vae.decode_uint8(z)                       # warm-up: allocator, tuning tables
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with TRACER.capturing(), torch.cuda.graph(g, capture_error_mode="thread_local"):
+                st.vae_img = self.vae.decode_uint8(z)
+            st.vae_graph = g
+        st.vae_graph.replay()
+        out = torch.empty_like(st.vae_img)
+        ops.copy_(out, st.vae_img)
+        return out
 
     @torch.no_grad()
     def denoise(self, ctx: torch.Tensor, latents: torch.Tensor, plan: SchedulePlan,
@@ -296,7 +326,7 @@ class StableDiffusion:
             self.last_latents = z
             if self.decode_stream is None:
                 with span("decode", self.stream):
-                    img = self.vae.decode_uint8(z)
+                    img = self._decode(st, z)
         out_stream = self.stream
         if self.decode_stream is not None:
             self.decode_stream.wait_stream(self.stream)

@@ -15,16 +15,15 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 
-def split_cus(total: int, reserve: int) -> Tuple[List[int], List[int]]:
-    """(reserved, rest): ``reserve`` CUs spread evenly over the id range (the CUs of one XCD are
-    contiguous ids, so this spreads the reservation over the XCDs and their L2s)."""
+def split_cus(total: int, reserve: int, n_xcd: int = 8) -> Tuple[List[int], List[int]]:
+    """(reserved, rest) as CU-mask bit ids.  The driver deals mask bits out round-robin over the
+    XCDs (bit i -> XCD i mod 8, CU i div 8 of it), so the first ``reserve`` bits take CUs from
+    every XCD evenly.  Measured on MI355X (profiles/r3_live_cumask.txt): 8 bits at stride 32 --
+    all on XCD 0 under that mapping, a quarter of its CUs -- cost 26 % of generation
+    throughput, because every full-chip kernel waits for its slowest XCD."""
     reserve = max(0, min(reserve, total - 1))
-    if reserve == 0:
-        return [], list(range(total))
-    step = total / reserve
-    mine = sorted({int(i * step) for i in range(reserve)})
-    rest = [c for c in range(total) if c not in set(mine)]
-    return mine, rest
+    mine = list(range(reserve))
+    return mine, list(range(reserve, total))
 
 
 def mask_words(cus: Sequence[int], total: int) -> List[int]:
@@ -43,9 +42,13 @@ def masked_stream(device, cus: Sequence[int]) -> "torch.cuda.ExternalStream":
     return torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
 
 
-def reserved_streams(device, reserve: int) -> Tuple[Optional["torch.cuda.ExternalStream"],
-                                                    Optional["torch.cuda.ExternalStream"]]:
-    """(scorer stream on ``reserve`` CUs, generation stream on the rest), or (None, None)."""
+def reserved_streams(device, reserve: int, exclusive: bool = False) -> Tuple[
+        Optional["torch.cuda.ExternalStream"], Optional["torch.cuda.ExternalStream"]]:
+    """(scorer stream, generation stream): generation is masked OFF ``reserve`` CUs, which stay
+    free for the scorer.  The scorer stream is None (the caller's own high-priority stream over
+    ALL CUs: an idle-GPU score keeps the whole chip, a score under load starts on the reserved
+    CUs at once); ``exclusive`` masks the scorer to the reserved CUs as well.  (None, None)
+    without a reservation."""
     if reserve <= 0 or torch.device(device).type != "cuda":
         return None, None
     from ..ops._ext import ext
@@ -53,4 +56,4 @@ def reserved_streams(device, reserve: int) -> Tuple[Optional["torch.cuda.Externa
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     total = int(ext().cu_count(idx))
     mine, rest = split_cus(total, reserve)
-    return masked_stream(device, mine), masked_stream(device, rest)
+    return (masked_stream(device, mine) if exclusive else None), masked_stream(device, rest)

@@ -795,8 +795,9 @@ def test_cu_masked_streams_run_kernels():
     kernels correctly, and a captured graph replays on the masked generation stream"""
     from cassmantle_amd.runtime.cumask import reserved_streams, split_cus
     mine, rest = split_cus(256, 8)
-    assert len(mine) == 8 and len(rest) == 248 and not set(mine) & set(rest)
-    s_score, s_gen = reserved_streams(DEV, 8)
+    assert mine == list(range(8)) and len(rest) == 248 and not set(mine) & set(rest)
+    assert reserved_streams(DEV, 8)[0] is None          # default: scorer keeps every CU
+    s_score, s_gen = reserved_streams(DEV, 8, exclusive=True)
     x = rnd(512, 640, seed=16)
     w = rnd(640, 640, scale=640 ** -0.5, seed=17)
     exp = ops.linear(x, w)
@@ -815,3 +816,15 @@ def test_cu_masked_streams_run_kernels():
         g.replay()
     s_gen.synchronize()
     assert torch.equal(y, exp)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 4096 + 7])
+def test_device_copy_kernel(n):
+    src = torch.randint(0, 255, (n,), device=DEV, dtype=torch.uint8)
+    dst = torch.zeros_like(src)
+    ops.copy_(dst, src)
+    assert torch.equal(dst, src)
+    a = rnd(77, 768, seed=21)
+    b = torch.empty_like(a)
+    ops.copy_(b, a)
+    assert torch.equal(a, b)

@@ -50,6 +50,10 @@ def parse():
                          "on the legacy default stream it queued behind whole generations, "
                          "pipeline.StableDiffusion.generate_tensor docstring)")
     ap.add_argument("--window-ms", type=float, default=1.0)
+    ap.add_argument("--switch-ms", type=float, default=None,
+                    help="sys.setswitchinterval for the process (ms); default: Python's 5 ms")
+    ap.add_argument("--exclusive-scorer", action="store_true",
+                    help="mask the scorer to the reserved CUs too (default: scorer on all CUs)")
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs reserved for the scorer (CU-masked streams, runtime/cumask.py); 0 = none")
     ap.add_argument("--score-topology", choices=("central", "sharded"), default="central",
@@ -88,13 +92,15 @@ def main():
     from cassmantle_amd.scoring.batcher import BatchingScorer
     from cassmantle_amd.scoring.encoder import EncoderBackend
 
+    if a.switch_ms is not None:
+        sys.setswitchinterval(a.switch_ms / 1e3)
     ctx = cdist.init_from_env()
     rank, world, dev = ctx.rank, ctx.world_size, ctx.device
     n_players = a.players if rank == 0 else 0          # rank-0-central scoring, as serve.py
     s_score = s_gen = None
     if a.reserve_cus > 0:
         from cassmantle_amd.runtime.cumask import reserved_streams
-        s_score, s_gen = reserved_streams(dev, a.reserve_cus)
+        s_score, s_gen = reserved_streams(dev, a.reserve_cus, exclusive=a.exclusive_scorer)
     sd = StableDiffusion(SPECS[a.model], device=dev, seed=0, stream=s_gen)
     backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority, stream=s_score)
     sharded = follower = None
@@ -116,6 +122,7 @@ def main():
 
     # warm everything (graph capture, allocator, scorer shapes)
     sd.generate_tensor(prompts(0), neg, list(range(a.batch))).cpu()
+    print(f"[live] warm generation done", file=sys.stderr, flush=True)
     if n_players:
         asyncio.run(run_players(scorer, min(n_players, 4), 1.0, a.think_ms, rank + 99))
     if dev.type == "cuda":
@@ -124,6 +131,7 @@ def main():
         torch.distributed.barrier()
 
     idle = asyncio.run(run_players(scorer, n_players, a.idle_s, a.think_ms, rank)) if n_players else []
+    print(f"[live] idle phase done: {len(idle)} requests", file=sys.stderr, flush=True)
 
     done = {"images": 0}
     stop = threading.Event()
@@ -135,6 +143,7 @@ def main():
             sd.generate(prompts(step), neg, [rank * 10000 + step * 10 + j for j in range(a.batch)])
             done["images"] += a.batch
             step += 1
+            print(f"[live] {done['images']} images", file=sys.stderr, flush=True)
 
     if world > 1:
         torch.distributed.barrier()
@@ -174,7 +183,8 @@ def main():
             "think_ms": a.think_ms, "idle_p50_ms": round(s[1], 3), "idle_p99_ms": round(s[2], 3),
             "load_p50_ms": round(s[3], 3), "load_p99_ms": round(s[4], 3), "requests": int(s[5]),
             "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
-            "score_topology": a.score_topology, "reserved_cus": a.reserve_cus,
+            "score_topology": a.score_topology, "reserved_cus": a.reserve_cus, "exclusive_scorer": a.exclusive_scorer,
+            "switch_ms": sys.getswitchinterval() * 1e3,
             "sharded_pairs": sharded.sharded_pairs if sharded is not None else 0,
             "config": {"model": a.model, "batch_per_room": a.batch, "graphs": bool(sd.use_graphs)}}), flush=True)
     cdist.shutdown()

@@ -44,6 +44,19 @@ def main():
     print(f"non-in-tree kernels: {sum(other.values())} launches of {len(other)} kinds")
     for k, n in other.most_common(30):
         print(f"  {n:6d}  {k}")
+    # the same census restricted to the LAST generation (everything after the previous image's
+    # to_uint8 up to the last one: encode, denoise, decode) -- model load / weight upload /
+    # capture-time copies fall outside it
+    ends = [i for i, r in enumerate(rows) if "to_uint8_kernel" in r["Kernel_Name"]]
+    if ends:
+        lo = ends[-2] + 1 if len(ends) > 1 else 0
+        win = rows[lo:ends[-1] + 1]
+        gen = collections.Counter(r["Kernel_Name"][:90] for r in win
+                                  if not ("anonymous namespace" in r["Kernel_Name"]
+                                          or r["Kernel_Name"].startswith(("attn_", "gemm_"))))
+        print(f"last generation: {len(win)} launches, non-in-tree: {sum(gen.values())} of {len(gen)} kinds")
+        for k, n in gen.most_common(30):
+            print(f"  {n:6d}  {k}")
 
 
 if __name__ == "__main__":
