@@ -195,14 +195,19 @@ class SelfAttention(nn.Module):
         self.to_qkv = Linear(dim, 3 * dim, bias=qkv_bias, gen=gen, dtype=dtype)
         self.to_out = Linear(dim, dim, bias=out_bias, gen=gen, dtype=dtype)
 
-    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False, qkv=None):
-        """``qkv``: the fused projection already computed (e.g. with a folded LayerNorm)."""
+    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False, qkv=None, kv8=None):
+        """``qkv``: the fused projection already computed (e.g. with a folded LayerNorm);
+        ``kv8``: its K/V as the fp8 attention image (ops.ln_linear(kv8=...)), fp8 only."""
         if qkv is None:
             qkv = self.to_qkv(x)
         B, N = qkv.shape[0], qkv.shape[1]
         C = self.dim
         qkv = qkv.view(B, N, 3, self.heads, self.head_dim)
-        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, kv_lens=kv_lens, fp8=fp8)
+        if kv8 is not None:
+            assert fp8 and kv_lens is None, "kv8: fp8 self-attention without key lengths"
+            o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, fp8=True, kv8=kv8)
+        else:
+            o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, kv_lens=kv_lens, fp8=fp8)
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
 

@@ -108,6 +108,9 @@ class ResnetBlock(nn.Module):
 # other K take a read-only row-statistics pass + epilogue correction.  On by default;
 # CASSMANTLE_LN_FOLD=0 restores LayerNorm kernel + plain GEMM.
 _LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "1") == "1"
+# fp8 self-attention K/V emitted by the QKV projection's epilogue (no per-call pack kernel);
+# CASSMANTLE_FP8_KV_EPILOGUE=0 restores the pack (A/B knob)
+_FP8_KV_EPILOGUE = os.environ.get("CASSMANTLE_FP8_KV_EPILOGUE", "1") == "1"
 
 
 class BasicTransformerBlock(nn.Module):
@@ -146,8 +149,12 @@ class BasicTransformerBlock(nn.Module):
             # read-only row-statistics pass each, no normalised activation in HBM
             f = self.folds()
             n1, n2, n3 = self.norm1, self.norm2, self.norm3
-            qkv = ops.ln_linear(x, n1.weight, n1.bias, n1.eps, self.attn1.to_qkv.weight, fold=f[0])
-            x = self.attn1(None, residual=x, fp8=fp8, qkv=qkv)
+            # fp8 (SDXL): the QKV epilogue writes K/V straight into the fp8 attention image
+            kv8 = None
+            if fp8 and _FP8_KV_EPILOGUE and ops.kv8_ok(x, self.attn1.head_dim):
+                kv8 = ops.kv8_image(x.shape[0], x.shape[1], x.shape[2], x.device)
+            qkv = ops.ln_linear(x, n1.weight, n1.bias, n1.eps, self.attn1.to_qkv.weight, fold=f[0], kv8=kv8)
+            x = self.attn1(None, residual=x, fp8=fp8, qkv=qkv, kv8=kv8)
             q = ops.ln_linear(x, n2.weight, n2.bias, n2.eps, self.attn2.to_q.weight, fold=f[1])
             x = self.attn2(None, ctx, residual=x, fp8=fp8, q=q)
             h = ops.ln_linear(x, n3.weight, n3.bias, n3.eps, self.ff.proj_in.weight, act="geglu", fold=f[2])

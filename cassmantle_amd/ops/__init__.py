@@ -202,15 +202,23 @@ LN_FOLD_MODE = int(os.environ.get("CASSMANTLE_LN_FOLD_MODE", "1"))
 
 def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], eps: float,
               w: torch.Tensor, bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
-              act: Optional[str] = None, fold=None) -> torch.Tensor:
+              act: Optional[str] = None, fold=None, kv8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``linear(layer_norm(x), w, bias, residual, act)``.  With ``fold`` (:func:`ln_fold` of these
     weights) on the HIP path the LayerNorm is folded into the GEMM: a read-only row-statistics
     pass, then the GEMM on the raw rows with the folded weights and a per-row epilogue
-    correction — the normalised activation is never written or re-read."""
+    correction — the normalised activation is never written or re-read.
+
+    ``kv8`` (x [B, N, C] -> fused Q|K|V [B, N, 3C] of 64-wide heads, N % 64 == 0): the epilogue
+    writes the K and V columns as the e4m3 image of the fp8 attention kernel (:func:`kv8_image`)
+    into ``kv8`` instead of bf16 (those columns of the result are then undefined): self-attention
+    needs no per-call pack."""
     K = x.shape[-1]
     rows = x.numel() // K
     if fold is None or not _use_hip(x) or rows <= 8 or K % 8 or (LN_FOLD_MODE == 2 and K not in (320, 640)):
-        return linear(layer_norm(x, ln_weight, ln_bias, eps), w, bias, residual=residual, act=act)
+        y = linear(layer_norm(x, ln_weight, ln_bias, eps), w, bias, residual=residual, act=act)
+        if kv8 is not None:
+            _pack_qkv8(y, kv8)
+        return y
     wf, wsum, bf = fold
     x2 = x.reshape(rows, K)
     if not x2.is_contiguous():
@@ -220,8 +228,30 @@ def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.
     r2 = residual.reshape(rows, N) if residual is not None else None
     # row statistics: inside the A-in-registers GEMM when it takes the shape (K = 320 / 640),
     # else one read-only stats pass chosen by the binding
-    _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps))
+    if kv8 is not None:
+        C = N // 3
+        _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps), kv8, C,
+                int(x.shape[-2]), C // 64)
+    else:
+        _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps))
     return out.reshape(*x.shape[:-1], N)
+
+
+def kv8_image(B: int, N: int, C: int, device) -> torch.Tensor:
+    """An (uninitialised) e4m3 K/V image for B images of N keys and C = 64 x heads channels."""
+    return torch.empty(2 * B * N * C, device=device, dtype=torch.uint8)
+
+
+def kv8_ok(x: torch.Tensor, head_dim: int) -> bool:
+    """Can :func:`ln_linear` emit the fp8 K/V image for self-attention over x [B, N, C]?"""
+    return _use_hip(x) and x.dim() == 3 and head_dim == 64 and x.shape[1] % 64 == 0 and x.shape[-1] % 64 == 0
+
+
+def _pack_qkv8(y: torch.Tensor, kv8: torch.Tensor) -> None:
+    B, N, C3 = y.shape
+    C = C3 // 3
+    qkv = y.view(B, N, 3, C // 64, 64)
+    pack_kv_fp8(qkv[:, :, 1], qkv[:, :, 2], out=kv8)
 
 
 def linear_cat(x: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -495,6 +525,20 @@ def pack_kv_fp8(k: torch.Tensor, v: torch.Tensor, kv_lens: Optional[torch.Tensor
         out = torch.empty(n, device=k.device, dtype=torch.uint8)
     ext().attention_fp8_pack(k, v, kv_lens, out)
     return out
+
+
+FP8_ATTN_VARIANTS = ("8x1", "4x1", "4x2", "2x2", "2x4", "1x4")
+
+
+def set_fp8_attention_variant(variant: Optional[str]) -> None:
+    """Force the fp8 attention kernel's block shape ("NQxNS": NQ query groups of 32 x NS key
+    splits per block; one of FP8_ATTN_VARIANTS) or restore the shape rule (None)."""
+    if variant is None:
+        ext().set_fp8_attn_variant(0)
+        return
+    assert variant in FP8_ATTN_VARIANTS, variant
+    nq, ns = (int(x) for x in variant.split("x"))
+    ext().set_fp8_attn_variant(nq * 10 + ns)
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,

@@ -549,18 +549,7 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
 constexpr int F8_KSTR = 80;   // LDS row stride (bytes) of the 64-byte fp8 rows: 16-lane groups
                               // of ds_read_b128 hit disjoint banks (20 r mod 64 distinct)
 
-CM_DEVICE uint32_t f8x4(float a, float b, float c, float d) {
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  return (uint32_t)w;
-}
-
-// slot of key offset kk (0..63) inside its 64-key block of V8t
-CM_DEVICE int f8_slot(int kk) {
-  const int hf = kk >> 5, w = kk & 31;
-  const int h = (w >> 2) & 1, r = (w & 3) + 4 * (w >> 3);
-  return 32 * h + 16 * hf + r;
-}
+// (f8x4 / f8_slot: common.h, shared with the GEMM epilogues that emit this image directly)
 
 // one block per (64-key tile, kv head, batch): K rows convert straight to K8 (8 B per thread,
 // 64-B rows); V goes through a 64 x 64-byte LDS image in the V8t slot order and leaves as
@@ -605,28 +594,70 @@ __global__ void __launch_bounds__(256) attn_fp8_pack_kernel(AttnArgs a, int Hk, 
 
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8,
-                                                           const uint8_t* __restrict__ V8t) {
-  constexpr int THREADS = 64 * NW;
-  constexpr int QB = 32 * NW;
+// Block = NQ query groups (32 queries each, one wave per group and key split) x NS key splits.
+// Wave (qg, ks) runs tiles ks, ks + NS, ks + 2 NS, ... of its group's keys, so each step stages
+// NS consecutive K/V tiles in LDS, each shared by the NQ waves of one split; at the end the
+// splits' partial (O, m, l) are merged through LDS by the ks = 0 wave.  NS > 1 is for the short
+// grids of SDXL (1024 queries x 20 heads x 2 CFG images = 1280 query groups for 1024 SIMDs: with
+// one split every wave walks all 16 key tiles at one wave per SIMD, a latency-bound chain);
+// splitting the keys multiplies the waves and divides the chain without a second kernel.
+// staging of one step's K/V tiles through registers: chunk slot I (0..3) of this thread as
+// plain variables (an array here was put in scratch memory by hipcc once LD > 1)
+#define F8_GSLOT(I, ST, KR, VR)                                                                  \
+  if constexpr (I < LD) {                                                                        \
+    const int c = tid + I * THREADS;                                                             \
+    if (c < CH) {                                                                                \
+      const int tt = c / (KT * 4), row = (c >> 2) % KT, cc = c & 3;                              \
+      const int t_ = (ST) * NS + tt;                                                             \
+      if (t_ < ntiles) {                                                                         \
+        KR = *reinterpret_cast<const uint4*>(Kg + (long long)(t_ * KT + row) * 64 + cc * 16);    \
+        VR = *reinterpret_cast<const uint4*>(Vg + (long long)row * Nkp + t_ * KT + cc * 16);     \
+      }                                                                                          \
+    }                                                                                            \
+  }
+#define F8_LSLOT(I, KR, VR)                                                                      \
+  if constexpr (I < LD) {                                                                        \
+    const int c = tid + I * THREADS;                                                             \
+    if (c < CH) {                                                                                \
+      const int tt = c / (KT * 4), row = (c >> 2) % KT, cc = c & 3;                              \
+      *reinterpret_cast<uint4*>(Ks + tt * TILE_B + row * F8_KSTR + cc * 16) = KR;                \
+      *reinterpret_cast<uint4*>(Vs + tt * TILE_B + row * F8_KSTR + cc * 16) = VR;                \
+    }                                                                                            \
+  }
+#define F8_GLOAD(ST) \
+  F8_GSLOT(0, ST, kr0, vr0) F8_GSLOT(1, ST, kr1, vr1) F8_GSLOT(2, ST, kr2, vr2) F8_GSLOT(3, ST, kr3, vr3)
+#define F8_LSTORE() F8_LSLOT(0, kr0, vr0) F8_LSLOT(1, kr1, vr1) F8_LSLOT(2, kr2, vr2) F8_LSLOT(3, kr3, vr3)
+
+template <int NQ, int NS>
+__global__ void __launch_bounds__(64 * NQ * NS, (NQ * NS >= 4) ? 8 / (NQ * NS) > 0 ? 8 / (NQ * NS) : 1 : 2)
+attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, const uint8_t* __restrict__ V8t) {
+  constexpr int NWV = NQ * NS;
+  constexpr int THREADS = 64 * NWV;
+  constexpr int QB = 32 * NQ;
   constexpr int TILE_B = KT * F8_KSTR;   // one 64-row fp8 tile in LDS
-  __shared__ __attribute__((aligned(16))) uint8_t Ks[TILE_B];
-  __shared__ __attribute__((aligned(16))) uint8_t Vs[TILE_B];
+  constexpr int STAGE_B = 2 * NS * TILE_B;
+  constexpr int MREC = 34;               // merge record per lane: 32 O registers, m, l
+  constexpr int MERGE_B = (NS - 1) * NQ * 64 * MREC * 4;
+  constexpr int LDS_B = STAGE_B > MERGE_B ? STAGE_B : MERGE_B;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_B];
+  uint8_t* const Ks = lds;
+  uint8_t* const Vs = lds + NS * TILE_B;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qg = wave % NQ, ks = wave / NQ;
   const int hlf = lane >> 5, ql = lane & 31;
   const int nqb = (a.Nq + QB - 1) / QB;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb, bh = bid / nqb;
   const int h = bh % a.H, b = bh / a.H;
   const int hk = a.group > 1 ? h / a.group : h;
-  const int q0 = qb * QB + wave * 32, q = q0 + ql;
+  const int q0 = qb * QB + qg * 32, q = q0 + ql;
 
   int nk = a.Nk;
   if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
   int ntiles = (nk + KT - 1) / KT;
   if (a.causal) ntiles = min(ntiles, (qb * QB + QB + KT - 1) / KT);
+  const int nsteps = (ntiles + NS - 1) / NS;
 
   // Q8 fragment: lane holds Q[q][32*hlf .. +31] * scale*log2e as e4m3
   i32x8_t qf;
@@ -645,32 +676,12 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel
   }
   const uint8_t* Kg = K8 + ((long long)b * Hk + hk) * Nkp * 64;
   const uint8_t* Vg = V8t + ((long long)b * Hk + hk) * 64 * Nkp;
-  // staging: 256 16-byte chunks per tile and operand (row = chunk >> 2, 4 chunks per row)
-  constexpr int LD = (KT * 4 + THREADS - 1) / THREADS;
-  uint4 kr[LD], vr[LD];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < LD; ++i) {
-      const int c = tid + i * THREADS;
-      if (c < KT * 4) {
-        const int row = c >> 2, cc = c & 3;
-        kr[i] = *reinterpret_cast<const uint4*>(Kg + (long long)(t * KT + row) * 64 + cc * 16);
-        vr[i] = *reinterpret_cast<const uint4*>(Vg + (long long)row * Nkp + t * KT + cc * 16);
-      }
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int i = 0; i < LD; ++i) {
-      const int c = tid + i * THREADS;
-      if (c < KT * 4) {
-        const int row = c >> 2, cc = c & 3;
-        *reinterpret_cast<uint4*>(Ks + row * F8_KSTR + cc * 16) = kr[i];
-        *reinterpret_cast<uint4*>(Vs + row * F8_KSTR + cc * 16) = vr[i];
-      }
-    }
-  };
-  if (ntiles > 0) { gload(0); lstore(); }
+  // staging: per step NS tiles x 256 16-byte chunks per operand (row = chunk >> 2, 4 per row)
+  constexpr int CH = NS * KT * 4;
+  constexpr int LD = (CH + THREADS - 1) / THREADS;
+  static_assert(LD <= 4, "fp8 attention staging: at most 4 chunks per thread");
+  uint4 kr0 = {}, kr1 = {}, kr2 = {}, kr3 = {}, vr0 = {}, vr1 = {}, vr2 = {}, vr3 = {};
+  if (nsteps > 0) { F8_GLOAD(0) F8_LSTORE() }
   __syncthreads();
 
   f32x16_t oacc[2];
@@ -680,86 +691,135 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m_run = 0.f, l_run = 0.f;
   constexpr float RESCALE_THR = 8.f;
+  const uint8_t* const Kw = Ks + ks * TILE_B;
+  const uint8_t* const Vw = Vs + ks * TILE_B;
 
-  for (int t = 0; t < ntiles; ++t) {
-    const bool more = t + 1 < ntiles;
-    if (more) gload(t + 1);
-    f32x16_t sacc[2];
+  for (int st = 0; st < nsteps; ++st) {
+    const bool more = st + 1 < nsteps;
+    if (more) { F8_GLOAD(st + 1) }
+    const int t = st * NS + ks;
+    if (t < ntiles) {                      // wave-uniform: the last step may not reach every split
+      f32x16_t sacc[2];
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
+      for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[hf][r] = -m_run;
-      const uint8_t* kp = Ks + (hf * 32 + ql) * F8_KSTR + 32 * hlf;
-      const uint4 k0 = *reinterpret_cast<const uint4*>(kp);
-      const uint4 k1 = *reinterpret_cast<const uint4*>(kp + 16);
-      const i32x8_t kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
-      sacc[hf] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, sacc[hf], 0, 0, 0, 127, 0, 127);
-    }
-    const int kbase = t * KT;
-    const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
-    if (need_mask) {
+        for (int r = 0; r < 16; ++r) sacc[hf][r] = -m_run;
+        const uint8_t* kp = Kw + (hf * 32 + ql) * F8_KSTR + 32 * hlf;
+        const uint4 k0 = *reinterpret_cast<const uint4*>(kp);
+        const uint4 k1 = *reinterpret_cast<const uint4*>(kp + 16);
+        const i32x8_t kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
+        sacc[hf] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, sacc[hf], 0, 0, 0, 127, 0, 127);
+      }
+      const int kbase = t * KT;
+      const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
+      if (need_mask) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kbase + hf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hlf;
+            if (key >= nk || (a.causal && key > q)) sacc[hf][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (__builtin_expect(st == 0 || !__all(mx <= RESCALE_THR), 0)) {
+        // a real branch: without the volatile asm hipcc if-converts this block and rescales O
+        // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
+        asm volatile("" ::: "memory");
+        float delta = (st == 0) ? mx : fmaxf(mx, 0.f);
+        if (!(delta > -1e30f)) delta = 0.f;
+        m_run += delta;
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[hf][r] -= delta;
+      }
+      float rs = 0.f;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int key = kbase + hf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hlf;
-          if (key >= nk || (a.causal && key > q)) sacc[hf][r] = -INFINITY;
+          const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
+          sacc[hf][r] = pv;
+          rs += pv;
         }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
-      // a real branch: without the volatile asm hipcc if-converts this block and rescales O
-      // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
-      asm volatile("" ::: "memory");
-      float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
-      if (!(delta > -1e30f)) delta = 0.f;
-      m_run += delta;
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      l_run *= alpha;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+      rs += __shfl_xor(rs, 32, 64);
+      l_run += rs;
+      // P^T fragment: element j = sacc[j >> 4][j & 15]
+      i32x8_t pf;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[hf][r] -= delta;
-    }
-    float rs = 0.f;
+        for (int c = 0; c < 4; ++c)
+          pf[4 * hf + c] = (int)f8x4(sacc[hf][4 * c], sacc[hf][4 * c + 1], sacc[hf][4 * c + 2], sacc[hf][4 * c + 3]);
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
-        sacc[hf][r] = pv;
-        rs += pv;
+      for (int dc = 0; dc < 2; ++dc) {
+        const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
+        const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
+        const i32x8_t vf = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+        oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
       }
-    rs += __shfl_xor(rs, 32, 64);
-    l_run += rs;
-    // P^T fragment: element j = sacc[j >> 4][j & 15]
-    i32x8_t pf;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        pf[4 * hf + c] = (int)f8x4(sacc[hf][4 * c], sacc[hf][4 * c + 1], sacc[hf][4 * c + 2], sacc[hf][4 * c + 3]);
-#pragma unroll
-    for (int dc = 0; dc < 2; ++dc) {
-      const uint8_t* vp = Vs + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
-      const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
-      const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
-      const i32x8_t vf = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
-      oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
     }
     __syncthreads();
     if (more) {
-      lstore();
+      F8_LSTORE()
       __syncthreads();
+    }
+  }
+  if constexpr (NS > 1) {
+    // merge the key splits: every wave is past the loop's last barrier, so the staging LDS is
+    // free; splits 1.. publish (O, m, l) per lane (lane-contiguous records: no bank conflicts)
+    float* const mg = reinterpret_cast<float*>(lds);
+    if (ks > 0) {
+      float* dst = mg + ((ks - 1) * NQ + qg) * 64 * MREC;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dst[r * 64 + lane] = oacc[0][r];
+        dst[(16 + r) * 64 + lane] = oacc[1][r];
+      }
+      dst[32 * 64 + lane] = m_run;
+      dst[33 * 64 + lane] = l_run;
+    }
+    __syncthreads();
+    if (ks > 0) return;                    // no barrier follows
+    // an empty split (no tile reached it, or every key masked) has l = 0 and takes no part
+    float mm = l_run > 0.f ? m_run : -INFINITY;
+#pragma unroll
+    for (int j = 1; j < NS; ++j) {
+      const float* src = mg + ((j - 1) * NQ + qg) * 64 * MREC;
+      if (src[33 * 64 + lane] > 0.f) mm = fmaxf(mm, src[32 * 64 + lane]);
+    }
+    if (mm > -INFINITY) {
+      const float a0 = l_run > 0.f ? __builtin_amdgcn_exp2f(m_run - mm) : 0.f;
+      l_run *= a0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= a0;
+#pragma unroll
+      for (int j = 1; j < NS; ++j) {
+        const float* src = mg + ((j - 1) * NQ + qg) * 64 * MREC;
+        const float lj = src[33 * 64 + lane];
+        const float aj = lj > 0.f ? __builtin_amdgcn_exp2f(src[32 * 64 + lane] - mm) : 0.f;
+        l_run = fmaf(aj, lj, l_run);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          oacc[0][r] = fmaf(aj, src[r * 64 + lane], oacc[0][r]);
+          oacc[1][r] = fmaf(aj, src[(16 + r) * 64 + lane], oacc[1][r]);
+        }
+      }
     }
   }
   if (q < a.Nq) {
@@ -778,6 +838,12 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : 2) attn_fp8_kernel
   }
 }
 
+template <int NQ, int NS>
+void launch_fp8_t(const AttnArgs& a, int Hk, int Nkp, const uint8_t* K8, const uint8_t* V8t, hipStream_t s) {
+  const int nqb = (a.Nq + 32 * NQ - 1) / (32 * NQ);
+  hipLaunchKernelGGL((attn_fp8_kernel<NQ, NS>), dim3(nqb * a.H * a.B), dim3(64 * NQ * NS), 0, s, a, Hk, Nkp, K8, V8t);
+}
+
 }  // namespace
 
 long long attention_fp8_workspace(const AttnArgs& a, int Hk) {
@@ -791,18 +857,39 @@ void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream
                      Nkp, ws, ws + (long long)a.B * Hk * Nkp * 64);
 }
 
+// forced fp8 variant NQ*10 + NS (0: the shape rule); set by ops.set_fp8_attention_variant
+static int g_fp8_attn_variant = 0;
+void set_fp8_attn_variant(int v) { g_fp8_attn_variant = v; }
+
 void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed) {
   const int Nkp = (a.Nk + KT - 1) / KT * KT;
   uint8_t* K8 = ws;
   uint8_t* V8t = ws + (long long)a.B * Hk * Nkp * 64;
   if (!packed) launch_attention_fp8_pack(a, Hk, ws, s);
-  const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
-  if (blocks8 >= 1024) {
-    const int nqb = (a.Nq + 255) / 256;
-    hipLaunchKernelGGL(attn_fp8_kernel<8>, dim3(nqb * a.H * a.B), dim3(512), 0, s, a, Hk, Nkp, K8, V8t);
-  } else {
-    const int nqb = (a.Nq + 127) / 128;
-    hipLaunchKernelGGL(attn_fp8_kernel<4>, dim3(nqb * a.H * a.B), dim3(256), 0, s, a, Hk, Nkp, K8, V8t);
+  // query groups of 32 over the chip's 1024 SIMDs: short grids split the keys too (NS), so
+  // every SIMD gets several waves.  CASSMANTLE_FP8_ATTN="NQxNS" forces a variant (A/B knob).
+  static const int env_forced = [] {
+    const char* e = getenv("CASSMANTLE_FP8_ATTN");
+    if (!e) return 0;
+    int nq = 0, ns = 0;
+    return sscanf(e, "%dx%d", &nq, &ns) == 2 ? nq * 10 + ns : 0;
+  }();
+  const int forced = g_fp8_attn_variant > 0 ? g_fp8_attn_variant : env_forced;
+  const long long groups = (long long)((a.Nq + 31) / 32) * a.H * a.B;
+  const int nkt = (a.Nk + KT - 1) / KT;
+  int v = forced;
+  // measured (tools/bench_attn_fp8.py, profiles/r3_attn_fp8_variants.jsonl): 2 query groups x
+  // 2 key splits is fastest at both SDXL self-attention shapes (1024 keys x 20 heads: 19.2 us vs
+  // 21.5 for 4x1; 4096 x 10: 84.5 vs 89.4); the 77-key cross-attention (2 tiles) keeps 4x1
+  if (v == 0) v = groups >= 8192 ? 81 : (nkt < 4 ? 41 : 22);
+  switch (v) {
+    case 81: return launch_fp8_t<8, 1>(a, Hk, Nkp, K8, V8t, s);
+    case 41: return launch_fp8_t<4, 1>(a, Hk, Nkp, K8, V8t, s);
+    case 22: return launch_fp8_t<2, 2>(a, Hk, Nkp, K8, V8t, s);
+    case 42: return launch_fp8_t<4, 2>(a, Hk, Nkp, K8, V8t, s);
+    case 14: return launch_fp8_t<1, 4>(a, Hk, Nkp, K8, V8t, s);
+    case 24: return launch_fp8_t<2, 4>(a, Hk, Nkp, K8, V8t, s);
+    default: return launch_fp8_t<4, 1>(a, Hk, Nkp, K8, V8t, s);
   }
 }
 

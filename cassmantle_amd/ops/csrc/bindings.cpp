@@ -65,7 +65,8 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
 void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act,
           const c10::optional<at::Tensor>& stats, int64_t stats_hw,
-          const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum, double ln_eps) {
+          const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum, double ln_eps,
+          const c10::optional<at::Tensor>& kv8, int64_t kv8_col0, int64_t kv8_ntok, int64_t kv8_hk) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
@@ -87,6 +88,17 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     CHECK_BF16(out);
   }
   p.C = out.data_ptr();
+  if (kv8.has_value() && kv8->defined()) {
+    // e4m3 K/V image of the fp8 attention kernel written by the epilogue (columns >= kv8_col0)
+    CHECK_DEV(*kv8); CHECK_CONTIG(*kv8);
+    TORCH_CHECK(kv8->scalar_type() == at::kByte && kv8_ntok > 0 && kv8_ntok % 64 == 0 && p.M % kv8_ntok == 0 &&
+                    kv8_hk > 0 && kv8_col0 % 8 == 0 && kv8_col0 + 128 * kv8_hk == p.N && act == 0 &&
+                    !p.out_f32 && !(residual.has_value() && residual->defined()) && !(stats.has_value() && stats->defined()),
+                "gemm kv8: uint8 image, 64-aligned tokens per image, K|V heads ending the output, plain epilogue");
+    TORCH_CHECK(kv8->numel() == 2LL * p.M * kv8_hk * 64, "gemm kv8: image size");
+    p.kv8 = kv8->data_ptr<uint8_t>();
+    p.kv8_col0 = (int)kv8_col0; p.kv8_ntok = (int)kv8_ntok; p.kv8_hk = (int)kv8_hk;
+  }
   if (stats.has_value() && stats->defined()) {
     TORCH_CHECK(stats_hw > 0 && p.M % stats_hw == 0, "gemm: stats_hw must divide the rows");
     p.stats_hw = (int)stats_hw;
@@ -717,7 +729,8 @@ PYBIND11_MODULE(_C, m) {
   // whole wait (~110 ms spikes in test_legacy_stream_scorer_not_blocked_by_generation).
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("out"),
         py::arg("act"), py::arg("stats"), py::arg("stats_hw"), py::arg("ln_rows") = py::none(),
-        py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0, nogil());
+        py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0, py::arg("kv8") = py::none(),
+        py::arg("kv8_col0") = 0, py::arg("kv8_ntok") = 0, py::arg("kv8_hk") = 0, nogil());
   m.def("row_stats", &row_stats, nogil());
   m.def("gemm_cat", &gemm_cat, nogil());
   m.def("group_norm_cat", &group_norm_cat, nogil());
@@ -753,6 +766,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("latent_init", &latent_init, nogil());
   m.def("finalize_latents", &finalize_latents, nogil());
   m.def("dcopy", &dcopy, nogil());
+  m.def("set_fp8_attn_variant", [](int64_t v) { set_fp8_attn_variant((int)v); });
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());

@@ -30,6 +30,46 @@ CM_DEVICE uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// four fp32 -> four OCP e4m3 bytes (little-endian)
+CM_DEVICE uint32_t f8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+// slot of key offset kk (0..63) inside its 64-key block of the fp8 attention kernel's V8t image
+// (attention.hip: slot 32h + j of a block holds the key of S accumulator register j&15 of key
+// half j>>4 in lane half h)
+CM_DEVICE int f8_slot(int kk) {
+  const int hf = kk >> 5, w = kk & 31;
+  const int h = (w >> 2) & 1, r = (w & 3) + 4 * (w >> 3);
+  return 32 * h + 16 * hf + r;
+}
+
+// e4m3 K/V emission (GemmArgs::kv8): stores final values o[0..3] of row m, columns n..n+3 into
+// the fp8 attention image when they are K or V columns; false for every other column
+template <class Args>   // GemmArgs (kernels.h)
+CM_DEVICE bool kv8_store4(const Args& p, int m, int n, const float* o) {
+  if (p.kv8 == nullptr || n < p.kv8_col0) return false;
+  const int C = p.kv8_hk * 64, rel = n - p.kv8_col0;
+  const int b = m / p.kv8_ntok, key = m - b * p.kv8_ntok;
+  const uint32_t w = f8x4(o[0], o[1], o[2], o[3]);
+  if (rel < C) {
+    const long long bh = (long long)b * p.kv8_hk + (rel >> 6);
+    *reinterpret_cast<uint32_t*>(p.kv8 + (bh * p.kv8_ntok + key) * 64 + (rel & 63)) = w;
+  } else {
+    const long long B = p.M / p.kv8_ntok;
+    uint8_t* V8t = p.kv8 + B * p.kv8_hk * p.kv8_ntok * 64;
+    const long long bh = (long long)b * p.kv8_hk + ((rel - C) >> 6);
+    const long long col = (key & ~63) + f8_slot(key & 63);
+    uint8_t* dst = V8t + (bh * 64 + ((rel - C) & 63)) * p.kv8_ntok + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[(long long)e * p.kv8_ntok] = (uint8_t)(w >> (8 * e));
+  }
+  return true;
+}
+
+
 CM_DEVICE void unpack8(const uint4& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
   f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);

@@ -338,7 +338,8 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
           for (int e = 0; e < 4; ++e) o[e] += r[e];
         }
         const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.C) + (long long)m * p.ldc + n) = pk;
+        if (GEGLU || !kv8_store4(p, m, n, o))
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.C) + (long long)m * p.ldc + n) = pk;
         if (!GEGLU && p.stats) {   // statistics of the STORED (bf16-rounded) values
           const float q0 = bf2f(pk.x & 0xffff), q1 = bf2f(pk.x >> 16), q2 = bf2f(pk.y & 0xffff), q3 = bf2f(pk.y >> 16);
           ssum[i][0] += q0; ssum[i][1] += q1; ssum[i][2] += q2; ssum[i][3] += q3;

@@ -105,6 +105,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
       for (int r = 0; r < 4; ++r) o[r] = apply_act(o[r], p.act);
     }
     if (p.residual) add4(o, *reinterpret_cast<const uint2*>(p.residual + om * p.ldc + n));
+    if (!OUTF32 && kv8_store4(p, m, n, o)) return;
     if constexpr (OUTF32) {
       float* C = reinterpret_cast<float*>(p.C) + (long long)batch * p.sC + om * p.ldc + n;
       *reinterpret_cast<float4*>(C) = make_float4(o[0], o[1], o[2], o[3]);
@@ -236,6 +237,13 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
 #pragma unroll
           for (int e = 0; e < 8; ++e) a[e] += b[e];
           v = pack8(a);
+        }
+        if (p.kv8 != nullptr && n >= p.kv8_col0) {   // K / V columns: e4m3 attention image only
+          float a[8];
+          unpack8(v, a);
+          kv8_store4(p, m, n, a);
+          kv8_store4(p, m, n + 4, a + 4);
+          return v;
         }
         *reinterpret_cast<uint4*>(Cb + om * p.ldc + n) = v;
         return v;

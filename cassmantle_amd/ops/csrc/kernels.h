@@ -47,6 +47,12 @@ struct GemmArgs {
   // stats_hw = rows per image
   long long* stats = nullptr;
   int stats_hw = 0;
+  // e4m3 K/V emission for the fp8 attention kernel (SDXL self-attention): output columns
+  // [kv8_col0, kv8_col0 + 128 kv8_hk) are the K then V heads (64 wide) of images of kv8_ntok
+  // tokens (kv8_ntok % 64 == 0); they are stored as K8 [B][Hk][ntok][64] and V8t [B][Hk][64][ntok]
+  // (slot-permuted key blocks) in kv8 instead of bf16 in C (attention.hip's packed image)
+  uint8_t* kv8 = nullptr;
+  int kv8_col0 = 0, kv8_ntok = 0, kv8_hk = 0;
 };
 #define GEMM_MAX_SPLIT 16
 struct GemmPlan { int cfg; int split; };
@@ -87,6 +93,7 @@ void launch_attention_d512(const AttnArgs& a, float* ws, hipStream_t s);
 long long attention_fp8_workspace(const AttnArgs& a, int Hk);
 // packed = true: ws already holds K8/V8t of these K/V (attention_fp8_pack once per text
 // context for cross-attention), only the attention kernel runs
+void set_fp8_attn_variant(int v);
 void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed = false);
 void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
 

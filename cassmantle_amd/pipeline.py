@@ -15,6 +15,7 @@ hot loop of the whole framework, so:
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 import time
 from dataclasses import dataclass
@@ -53,6 +54,10 @@ SPECS: Dict[str, PipelineSpec] = {
 
 def default_device() -> torch.device:
     return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+# VAE decode captured as a graph per step state (CASSMANTLE_VAE_GRAPH=0: eager, A/B knob)
+_VAE_GRAPH = os.environ.get("CASSMANTLE_VAE_GRAPH", "1") == "1"
 
 
 class _StepState:
@@ -233,7 +238,7 @@ class StableDiffusion:
         captured once per state and replayed (~200 eager launches per generation otherwise: host
         time that also holds the GIL against a serving process's scorer thread); the replay's
         static output is copied out, so the returned image outlives the next generation."""
-        if not self.use_graphs or z is not st.z:
+        if not self.use_graphs or not _VAE_GRAPH or z is not st.z:
             return self.vae.decode_uint8(z)
         if st.vae_graph is None:
             s = torch.cuda.Stream(device=self.device)

@@ -371,6 +371,28 @@ def test_attention_fp8(B, Nq, Nk, H, causal, lens):
     assert torch.isfinite(out8.float()).all()
 
 
+@pytest.mark.parametrize("variant", ["8x1", "4x1", "4x2", "2x2", "2x4", "1x4"])
+@pytest.mark.parametrize("B,Nq,Nk,H,causal,lens", [(2, 1024, 1024, 20, False, None), (3, 300, 300, 4, True, None),
+                                                   (3, 200, 130, 2, False, [130, 65, 3]),
+                                                   (2, 256, 77, 4, False, [77, 5])])
+def test_attention_fp8_block_variants(variant, B, Nq, Nk, H, causal, lens):
+    """every fp8 block shape (NQ query groups x NS key splits merged through LDS) against the
+    fp32 reference, including splits that get no tile (short / ragged / causal key ranges)"""
+    d = 64
+    q = rnd(B, Nq, H, d, scale=2.0, seed=46)
+    k = rnd(B, Nk, H, d, seed=47)
+    v = rnd(B, Nk, H, d, seed=48)
+    kl = torch.tensor(lens, dtype=torch.int32, device=DEV) if lens else None
+    exp = ref.attention(q, k, v, causal=causal, kv_lens=kl)
+    ops.set_fp8_attention_variant(variant)
+    try:
+        out = ops.attention(q, k, v, causal=causal, kv_lens=kl, fp8="force")
+    finally:
+        ops.set_fp8_attention_variant(None)
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out, exp) < 0.12, rel_err(out, exp)
+
+
 @pytest.mark.parametrize("B,Nq,Nk,H,lens", [(2, 4096, 77, 10, None), (2, 1024, 77, 20, None),
                                           (3, 200, 130, 2, [130, 65, 3])])
 def test_attention_fp8_prepacked_kv(B, Nq, Nk, H, lens):
@@ -828,3 +850,35 @@ def test_device_copy_kernel(n):
     b = torch.empty_like(a)
     ops.copy_(b, a)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,C,split", [(1024, 1280, 0), (1024, 1280, 2), (4096, 640, 0), (256, 640, 0)])
+def test_qkv_epilogue_emits_fp8_kv(N, C, split):
+    """SDXL fp8 self-attention: the LayerNorm-folded QKV GEMM writes K/V straight into the fp8
+    attention image (row-stats + LDS-staged epilogue at C = 1280, split-K reduce epilogue with
+    split 2, in-kernel-LN A-in-registers epilogue at C = 640).  Q columns are bit-identical to the
+    plain projection; the image matches the per-call pack of the bf16 K/V except for double-
+    rounding ties (fp32 -> e4m3 directly vs via bf16), and the attention outputs agree."""
+    from cassmantle_amd.ops._ext import ext
+    B, H = 2, C // 64
+    x = rnd(B, N, C, seed=60)
+    lw = (rnd(C, scale=0.3, seed=61).float() + 1.0).to(torch.bfloat16)
+    lb = rnd(C, scale=0.1, seed=62)
+    w = rnd(3 * C, C, scale=C ** -0.5, seed=63)
+    fold = ops.ln_fold(lw, lb, w)
+    plain = ops.ln_linear(x, lw, lb, 1e-5, w, fold=fold).view(B, N, 3, H, 64)
+    kv8 = ops.kv8_image(B, N, C, DEV)
+    if split:
+        ext().gemm_set_override(-1, split)
+    try:
+        qkv = ops.ln_linear(x, lw, lb, 1e-5, w, fold=fold, kv8=kv8).view(B, N, 3, H, 64)
+    finally:
+        if split:
+            ext().gemm_set_override(-1, 0)
+    assert torch.equal(qkv[:, :, 0], plain[:, :, 0])
+    pk = ops.pack_kv_fp8(plain[:, :, 1], plain[:, :, 2])
+    assert pk.numel() == kv8.numel()
+    assert (pk != kv8).float().mean().item() < 0.02
+    o1 = ops.attention(plain[:, :, 0], plain[:, :, 1], plain[:, :, 2], fp8=True, kv8=kv8)
+    o2 = ops.attention(plain[:, :, 0], plain[:, :, 1], plain[:, :, 2], fp8=True, kv8=pk)
+    assert rel_err(o1, o2) < 0.02
