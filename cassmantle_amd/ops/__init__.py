@@ -244,7 +244,10 @@ def kv8_image(B: int, N: int, C: int, device) -> torch.Tensor:
 
 def kv8_ok(x: torch.Tensor, head_dim: int) -> bool:
     """Can :func:`ln_linear` emit the fp8 K/V image for self-attention over x [B, N, C]?"""
-    return _use_hip(x) and x.dim() == 3 and head_dim == 64 and x.shape[1] % 64 == 0 and x.shape[-1] % 64 == 0
+    # (C = 320 / 640 run the A-in-registers GEMM, whose epilogue stores straight from the
+    # accumulators: no LDS tile to transpose V through, so those keep the per-call pack)
+    return (_use_hip(x) and x.dim() == 3 and head_dim == 64 and x.shape[1] % 64 == 0 and x.shape[-1] % 64 == 0
+            and x.shape[-1] not in (320, 640))
 
 
 def _pack_qkv8(y: torch.Tensor, kv8: torch.Tensor) -> None:

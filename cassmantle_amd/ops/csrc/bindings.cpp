@@ -46,6 +46,9 @@ void run_gemm(GemmArgs& p, const at::Tensor& like) {
   const GemmPlan plan = gemm_plan(p);
   p.cfg = plan.cfg;
   p.split = plan.split;
+  // fp8 K/V emission runs in the LDS-staged epilogue (V transposed through the tile in LDS);
+  // the split-K reduce would scatter V byte by byte
+  if (p.kv8 != nullptr) p.split = 1;
   long long* post_stats = nullptr;
   if (p.stats != nullptr && (p.out_f32 || p.M <= 8 || (p.batch != 1 && !p.parity) || p.act == 4 || p.act == 6)) {
     post_stats = p.stats;

@@ -239,10 +239,14 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
           v = pack8(a);
         }
         if (p.kv8 != nullptr && n >= p.kv8_col0) {   // K / V columns: e4m3 attention image only
-          float a[8];
-          unpack8(v, a);
-          kv8_store4(p, m, n, a);
-          kv8_store4(p, m, n + 4, a + 4);
+          if (n < p.kv8_col0 + 64 * p.kv8_hk) {       // K: 8 bytes of key m's 64-byte row
+            float a[8];
+            unpack8(v, a);
+            const int rel = n - p.kv8_col0, b = m / p.kv8_ntok, key = m - b * p.kv8_ntok;
+            const long long bh = (long long)b * p.kv8_hk + (rel >> 6);
+            *reinterpret_cast<uint2*>(p.kv8 + (bh * p.kv8_ntok + key) * 64 + (rel & 63)) =
+                make_uint2(f8x4(a[0], a[1], a[2], a[3]), f8x4(a[4], a[5], a[6], a[7]));
+          }                                            // V: transposed pass below
           return v;
         }
         *reinterpret_cast<uint4*>(Cb + om * p.ldc + n) = v;
@@ -253,6 +257,36 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
           const int row = c / CPR, c8 = c - row * CPR;
           if (m0 + row >= p.M || n0 + c8 * 8 >= p.N) continue;
           finish(row, c8);
+        }
+        if (p.kv8 != nullptr && n0 + OBN > p.kv8_col0 + 64 * p.kv8_hk) {
+          // V columns -> V8t rows: d-row of a 64-key block = 64 slot-ordered bytes, written as
+          // 16-byte runs of 16 slots gathered from the bf16 tile in LDS (key blocks never
+          // straddle images: tokens per image and BM are multiples of 64)
+          const int vc0 = p.kv8_col0 + 64 * p.kv8_hk;
+          const long long Bimg = p.M / p.kv8_ntok;
+          uint8_t* V8t = p.kv8 + Bimg * p.kv8_hk * p.kv8_ntok * 64;
+          for (int it = tid; it < OBN * (BM / 64) * 4; it += THREADS) {
+            const int col = it % OBN, sg = (it / OBN) & 3, kb = it / (OBN * 4);
+            const int n = n0 + col, mb = m0 + kb * 64;
+            if (n < vc0 || n >= p.N || mb >= p.M) continue;
+            uint32_t w[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              float f[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int j = sg * 16 + q4 * 4 + e;           // slot 32h + j' of the block
+                const int h = j >> 5, jj = j & 31;
+                const int kk = 32 * (jj >> 4) + (jj & 3) + 8 * ((jj & 15) >> 2) + 4 * h;
+                f[e] = bf2f(T[(kb * 64 + kk) * OST + col]);
+              }
+              w[q4] = f8x4(f[0], f[1], f[2], f[3]);
+            }
+            const int b = mb / p.kv8_ntok, key0 = mb - b * p.kv8_ntok;
+            const long long bh = (long long)b * p.kv8_hk + ((n - vc0) >> 6);
+            *reinterpret_cast<uint4*>(V8t + (bh * 64 + ((n - vc0) & 63)) * p.kv8_ntok + key0 + sg * 16) =
+                make_uint4(w[0], w[1], w[2], w[3]);
+          }
         }
         return;
       }

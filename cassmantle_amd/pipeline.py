@@ -56,8 +56,10 @@ def default_device() -> torch.device:
     return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
 
 
-# VAE decode captured as a graph per step state (CASSMANTLE_VAE_GRAPH=0: eager, A/B knob)
-_VAE_GRAPH = os.environ.get("CASSMANTLE_VAE_GRAPH", "1") == "1"
+# VAE decode captured as a graph per step state: OFF by default -- measured slower than the eager
+# decode (13.5 vs 11.1 ms per 4-image decode, 558-560 vs 557-558 ms/step, same box x2,
+# profiles/r3_vae_graph_ab.txt); CASSMANTLE_VAE_GRAPH=1 turns it on
+_VAE_GRAPH = os.environ.get("CASSMANTLE_VAE_GRAPH", "0") == "1"
 
 
 class _StepState:

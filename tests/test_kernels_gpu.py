@@ -855,8 +855,9 @@ def test_device_copy_kernel(n):
 @pytest.mark.parametrize("N,C,split", [(1024, 1280, 0), (1024, 1280, 2), (4096, 640, 0), (256, 640, 0)])
 def test_qkv_epilogue_emits_fp8_kv(N, C, split):
     """SDXL fp8 self-attention: the LayerNorm-folded QKV GEMM writes K/V straight into the fp8
-    attention image (row-stats + LDS-staged epilogue at C = 1280, split-K reduce epilogue with
-    split 2, in-kernel-LN A-in-registers epilogue at C = 640).  Q columns are bit-identical to the
+    attention image (row-stats + LDS-staged epilogue at C = 1280, V transposed through the
+    tile in LDS; a forced split-K is overridden -- kv8 GEMMs never split; in-kernel-LN
+    A-in-registers epilogue at C = 640, which ops.kv8_ok leaves to the pack in the UNet).  Q columns are bit-identical to the
     plain projection; the image matches the per-call pack of the bf16 K/V except for double-
     rounding ties (fp32 -> e4m3 directly vs via bf16), and the attention outputs agree."""
     from cassmantle_amd.ops._ext import ext
@@ -878,7 +879,14 @@ def test_qkv_epilogue_emits_fp8_kv(N, C, split):
     assert torch.equal(qkv[:, :, 0], plain[:, :, 0])
     pk = ops.pack_kv_fp8(plain[:, :, 1], plain[:, :, 2])
     assert pk.numel() == kv8.numel()
-    assert (pk != kv8).float().mean().item() < 0.02
+    # fp32 -> e4m3 rounds once, fp32 -> bf16 -> e4m3 twice: they may differ by one code (an
+    # e4m3 ulp) where the bf16 rounding lands on an e4m3 tie (measured ~3 % of the bytes)
+    diff = (pk.int() - kv8.int()).abs()
+    assert (diff != 0).float().mean().item() < 0.06
+    assert diff.max().item() <= 1
     o1 = ops.attention(plain[:, :, 0], plain[:, :, 1], plain[:, :, 2], fp8=True, kv8=kv8)
     o2 = ops.attention(plain[:, :, 0], plain[:, :, 1], plain[:, :, 2], fp8=True, kv8=pk)
-    assert rel_err(o1, o2) < 0.02
+    exp = ref.attention(plain[:, :, 0], plain[:, :, 1], plain[:, :, 2])
+    # one-ulp e4m3 differences in ~3 % of K/V move the output by fp8 noise (2.7 % at 256 keys)
+    assert rel_err(o1, o2) < 0.05
+    assert rel_err(o1, exp) < 0.12 and rel_err(o2, exp) < 0.12
