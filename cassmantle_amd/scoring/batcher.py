@@ -70,7 +70,12 @@ class BatchingScorer(Scorer):
 
     async def _delayed_flush(self):
         await asyncio.sleep(self.window)
-        await self._flush()
+        # drain: requests that arrived while a batch was on the device are flushed as soon as it
+        # returns.  (A single flush stranded them until some later request started a new
+        # flusher: a scorer tail of several ms at idle, and a hang once every player was waiting
+        # on a stranded request -- tools/bench_live.py --switch-ms 0.5, profiles/r3_live_cumask.txt)
+        while self._queue:
+            await self._flush()
 
     def _run(self, flat):
         with self._lock:

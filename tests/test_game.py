@@ -317,6 +317,35 @@ def test_batching_scorer_merges_requests():
     run(main())
 
 
+def test_batching_scorer_flushes_requests_queued_during_a_batch():
+    """a request that arrives while the previous batch is on the device is flushed when that
+    batch returns -- not stranded until some later request happens to start a new flusher
+    (with no later request it waited forever: the live-round hang at a 0.5 ms GIL interval)"""
+    import time as _time
+
+    class SlowBackend:
+        def __init__(self, be):
+            self.be = be
+
+        def __getattr__(self, name):
+            return getattr(self.be, name)
+
+        def similarity(self, g, a):
+            _time.sleep(0.05)
+            return self.be.similarity(g, a)
+
+    async def main():
+        sc = _TableScorer()
+        b = BatchingScorer(SlowBackend(sc.backend), 0.01, window_ms=1)
+        first = asyncio.ensure_future(b.score([("lamp", "lantern")]))
+        await asyncio.sleep(0.02)                     # the first batch is now in flight
+        t0 = _time.perf_counter()
+        second = await asyncio.wait_for(b.score([("river", "river")]), timeout=2.0)
+        assert (await first)[0] > 0.9 and second[0] == 1.0
+        assert _time.perf_counter() - t0 < 0.5 and b.batches == 2
+    run(main())
+
+
 def test_wordvec_most_similar():
     sc = _TableScorer()
     res = sc.backend.most_similar("lantern", topn=3)
