@@ -142,7 +142,11 @@ class Conv2d(nn.Module):
         if self.pad_in > self.cin:
             self.padded_weight(self.pad_in)
 
-    def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None):
+    def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None, out=None):
+        if out is not None:         # (the UNet's conv_out writing one branch's rows of eps)
+            w = self.padded_weight(x.shape[-1]) if x.shape[-1] > self.cin else self.weight
+            return ops.conv2d(x, w, self.bias, self.stride, self.padding, residual=residual,
+                              upsample=upsample, chan_bias=chan_bias, stats=stats, out=out)
         if x.shape[-1] > self.cin:
             # input carries zero padding channels (graph-static UNet input): padded weights,
             # cached, instead of a pad copy of input and weight on every call

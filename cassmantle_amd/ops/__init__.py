@@ -301,9 +301,11 @@ def _torch_linear(x, w, bias, residual, act):
 # ----------------------------------------------------------------------------- conv (K4/K5/K12)
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
            padding: int = 1, residual: Optional[torch.Tensor] = None, upsample: bool = False,
-           chan_bias: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+           chan_bias: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NHWC implicit-GEMM convolution.  x [B,H,W,Cin], w [Cout,kh,kw,Cin].  ``stats``: see
-    :func:`linear` (per-(image, Cout) output statistics for a following GroupNorm)."""
+    :func:`linear` (per-(image, Cout) output statistics for a following GroupNorm).  ``out``: a
+    contiguous [B,Ho,Wo,Cout] buffer of x's dtype to write into (else a new tensor)."""
     if not _use_hip(x):
         if x.device.type == "cuda":
             y = _torch_conv(x, w, bias, stride, padding, residual, upsample, chan_bias)
@@ -311,7 +313,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             y = ref.conv2d(x, w, bias, stride, padding, residual, upsample, chan_bias)
         if stats is not None:
             channel_stats_ref(y, stats)
-        return y
+        return y if out is None else out.copy_(y)
     B, H, W, Cin = x.shape
     Cout, kh, kw, _ = w.shape
     if Cin % 8 != 0:
@@ -324,7 +326,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
     Ho = (Hi + 2 * padding - kh) // stride + 1
     Wo = (Wi + 2 * padding - kw) // stride + 1
-    out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=x.dtype)
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=x.dtype)
+    else:
+        assert out.shape == (B, Ho, Wo, Cout) and out.dtype == x.dtype and out.is_contiguous(), "conv2d: bad out"
     _launch(ext().conv2d, x.contiguous(), w, bias, residual, chan_bias, out, stride, padding, int(upsample), stats)
     return out
 
