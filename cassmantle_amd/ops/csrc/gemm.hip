@@ -41,12 +41,15 @@ constexpr int BK = 64;
 //       (M = 8192 x N = 640: 256 tiles)
 //   21: ping-pong 128x128 (4x2 waves, wave 32x64, 64 KiB LDS: 2 blocks per CU)
 //   22 / 23: ping-pong 128x64 / 256x64 (4x2 waves, 48 / 80 KiB LDS)
+//   24 / 25: halo-staged 3x3 conv 256x160 / 128x160 (gemm_halo.h: one halo tile per 64-channel
+//       chunk serves all 9 taps; half the LDS-DMA bytes per k-tile of the CONV 2 path)
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 24;
+constexpr int kNumTiles = 26;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
 constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22 || c == 23; }
+constexpr bool is_halo_cfg(int c) { return c == 24 || c == 25; }
 constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
 constexpr int kFirstDeep = 11;
@@ -60,7 +63,8 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 768},
                                        {128, 128, 1.f, 512},   {128, 160, 1.f, 512},   {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512}};
+                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512},
+                                       {256, 160, 1.f, 256},   {128, 160, 1.f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample
@@ -228,7 +232,8 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     // a table entry is only taken if the kernel family can run this call (same checks as a
     // forced config), so a stale table never selects an unsupported path
     const bool elig = tp.cfg < kFirstPP ||
-                      (is_pp_cfg(tp.cfg) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p) : deep_ok(p)));
+                      (is_pp_cfg(tp.cfg) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p)
+                                                       : is_halo_cfg(tp.cfg) ? gemm_halo_ok(p, tp.cfg) : deep_ok(p)));
     if (have && elig) return tp;
   }
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
@@ -242,6 +247,12 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   const bool deep_elig = deep_ok(p);
   if (force_cfg == kAreg) {
     if (gemm_areg_ok(p)) return GemmPlan{kAreg, 1};
+  } else if (is_halo_cfg(force_cfg)) {
+    if (gemm_halo_ok(p, force_cfg)) {
+      const int nch = p.Cin / 64;
+      const int sp = force_split > 0 ? force_split : 1;
+      if (sp <= nch && sp <= GEMM_MAX_SPLIT && (sp == 1 || p.N % 4 == 0)) return GemmPlan{force_cfg, sp};
+    }
   } else if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
       (force_cfg < kFirstPP || (is_pp_cfg(force_cfg) ? pp_elig : deep_elig))) {
     if (gated) {
@@ -307,6 +318,10 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     return;
   }
   const bool buf = buf_ok(p);
+  if (is_halo_cfg(p.cfg) && gemm_halo_ok(p, p.cfg)) {
+    gemm_halo_launch(p, ws, s);
+    return;
+  }
   if (p.cfg == kAreg && gemm_areg_ok(p)) {
     launch_gemm_areg(p, s);
     return;
