@@ -1,13 +1,9 @@
 // Halo-staged 3x3 convolution on the ping-pong 8-wave MFMA mainloop (the
 // UNet / VAE 3x3 convs, reference hot loop /root/reference/src/backend.py:270-295).
 //
-// Why: the ping-pong implicit-GEMM conv (gemm_pp.h CONV 2) stages, for every 64-deep k-tile
-// (one tap x 64 input channels), the BM shifted input rows of that tap plus BN weight rows by
-// LDS-DMA.  Measured on MI355X (profiles/r3_dma_bound.txt), every GEMM-family kernel here moves
-// ~20-22 B/cycle/CU by LDS-DMA whatever its tile (4096^3: 64 KB/k-tile in ~3300 cycles; level-1
-// conv 256x160: 52 KB in ~2700; 128x80: 26 KB in ~1180) and the level-1 conv is 20 % faster with
-// its DMA removed: the conv is bound by DMA bytes per k-tile, and 8 of every 9 A rows it stages
-// are the neighbouring tap's rows again.
+// Why it exists: the ping-pong implicit-GEMM conv (gemm_pp.h CONV 2) stages, for every 64-deep
+// k-tile (one tap x 64 input channels), the BM shifted input rows of that tap plus BN weight rows
+// by LDS-DMA, so 8 of every 9 A rows it stages are a neighbouring tap's rows again.
 //
 // What: a block owns BM output pixels that are whole output rows of one image (BM % Wo == 0);
 // per 64-channel chunk c it stages ONE halo tile -- the (BM/Wo + 2) x (Wo + 2) input pixels
@@ -15,6 +11,10 @@
 // the chunk's 9 taps as 9 k-tiles whose A fragments are read from the halo at a per-tap row
 // offset ky (Wo + 2) + kx.  Per k-tile the DMA carries BN weight rows plus 1/9 of a halo:
 // 25.6 KB instead of 52 KB at 256x160 on the 64^2 level.
+//
+// Measured (profiles/r3_bench_halo.jsonl, profiles/r3_dma_bound.txt): NOT faster than the CONV-2
+// tiles on any SD-1.5 shape (level-1 68.9 vs 65.4 us): the convs are not bound by DMA bytes.
+// Kept as opt-in tile configs 24/25 that the autotuner weighs for every shape.
 //
 // Pipeline (two phases per k-tile, as gemm_pp.h SCHED 2): P0 reads the W-a and all A fragments of
 // k-tile t and issues W of t+1 into the other W buffer; P1 reads W-b of t and issues ONE 64-row
