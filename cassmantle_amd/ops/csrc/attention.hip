@@ -43,7 +43,14 @@ struct AttnGeom {
 // PIPE (implies 3 K/V buffers): software-pipelined tiles -- the QK^T MFMAs of tile t + 1 are
 // issued before the softmax of tile t, so the matrix pipe works while the VALU runs the exps;
 // tiles are staged two ahead
-template <int DQK, int DO, int NW, bool DB, bool PIPE = false>
+// STAG (implies 3 K/V buffers, tiles staged two ahead): two barriers per tile -- after the
+// QK^T + softmax half and after the P.V half -- with waves NW/2.. one barrier behind, so on every
+// SIMD one wave's softmax VALU runs beside its partner's P.V MFMAs instead of both waves of a SIMD
+// doing the same half at once (the per-tile barrier of the DB loop keeps them in lock-step).
+// Hazards: tile t+2 is stored during the P.V half of t into the buffer of t-1, whose last reader
+// (a late wave's P.V of t-1) passed its barrier before any early wave starts the P.V half of t;
+// an early wave reads tile t+2 after the late waves' P.V-half barrier of t+1 > their stores.
+template <int DQK, int DO, int NW, bool DB, bool PIPE = false, bool STAG = false>
 // min blocks 8 / NW caps the kernel at 256 registers: the compiler then keeps the MFMA
 // accumulators in VGPRs, where the softmax reads and writes them (with a 512-register budget it
 // chose AGPRs and paid a v_accvgpr_read + write per score per pass: ~144 of ~300 VALU per tile)
@@ -176,7 +183,17 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     gload(0);
     lstore(0);
   }
+  const bool late = STAG && wave >= NW / 2;
+  if constexpr (STAG) {
+    if (ntiles > 1) {
+      gload(1);
+      lstore(BUF);
+    }
+  }
   __syncthreads();
+  if constexpr (STAG) {
+    if (late) __builtin_amdgcn_s_barrier();
+  }
 
   // tr-read lane geometry (T10): group g = lane>>4, i = lane&15 -> row q' = i>>2, col 4*(i&3)
   const int tg = lane >> 4, ti = lane & 15;
@@ -313,11 +330,12 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
       if (t + 1 >= ntiles) break;
       step(s1, s0, t + 1);
     }
-  } else
+  } else {
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
-    if (more) gload(t + 1);
-    const int bo = DB ? (t & 1) * BUF : 0;   // this tile's buffer
+    const bool ahead = STAG ? t + 2 < ntiles : more;      // a tile is staged during this one
+    if (ahead) gload(STAG ? t + 2 : t + 1);
+    const int bo = STAG ? (t % 3) * BUF : (DB ? (t & 1) * BUF : 0);   // this tile's buffer
 
     // ---- S^T = K Q^T for 64 keys (two 32-key accumulators)
     f32x16_t sacc[2];
@@ -420,6 +438,12 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
         pf[2 * hf + s] = as_bf16x8(u);
       }
 
+    if constexpr (STAG) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+    }
     // ---- O^T += V^T P^T
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -437,7 +461,13 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
       }
     }
 
-    if constexpr (DB) {
+    if constexpr (STAG) {
+      __builtin_amdgcn_s_setprio(0);
+      if (ahead) lstore(((t + 2) % 3) * BUF);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else if constexpr (DB) {
       // the other buffer was last read in tile t - 1, which every wave finished before the
       // previous barrier
       if (more) lstore(BUF - bo);
@@ -449,6 +479,10 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
         __syncthreads();
       }
     }
+  }
+  if constexpr (STAG) {
+    if (!late) __builtin_amdgcn_s_barrier();   // re-align the two halves
+  }
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l
@@ -490,6 +524,21 @@ void launch_t(const AttnArgs& a, hipStream_t s) {
   // CASSMANTLE_ATTN_DB=0|1: single / double-buffered K/V (A/B knob; double by default: level-1
   // self-attention 247 -> 240 us, 568.7 -> 566.7 ms/step same box x3, profiles/r2_attn_db_ab.txt)
   static const int db = [] { const char* e = getenv("CASSMANTLE_ATTN_DB"); return e ? atoi(e) : 1; }();
+  if constexpr (NW >= 4 && DO <= 96) {   // (the larger head dims spill in this variant)
+    if (db == 3) {
+      // CASSMANTLE_ATTN_DB=3: staggered waves on 3 K/V buffers (attn_fwd_kernel STAG)
+      auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true, false, true>;
+      if constexpr (3 * G::LDS_BYTES > 65536) {
+        static const bool once = [&] {
+          (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * G::LDS_BYTES);
+          return true;
+        }();
+        (void)once;
+      }
+      hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 3 * G::LDS_BYTES, s, a);
+      return;
+    }
+  }
   if constexpr (DQK <= 64) {
     if (db == 2) {
     // CASSMANTLE_ATTN_DB=2: software-pipelined tiles on 3 K/V buffers (head dims <= 64: the
@@ -526,7 +575,10 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
   // enough workgroups to fill 256 CUs: fall back to fewer waves per block for short sequences
   long long blocks4 = (long long)((a.Nq + 127) / 128) * a.H * a.B;
   long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
-  if (DO <= 96 && blocks8 >= 1024) launch_t<DQK, DO, 8>(a, s);   // 8 waves share each K/V tile
+  // CASSMANTLE_ATTN_NW=4: never the 8-wave block (A/B knob: two 4-wave blocks per CU are not
+  // lock-stepped by one block's per-tile barrier, at twice the K/V tile loads)
+  static const int nw_cap = [] { const char* e = getenv("CASSMANTLE_ATTN_NW"); return e ? atoi(e) : 8; }();
+  if (DO <= 96 && blocks8 >= 1024 && nw_cap >= 8) launch_t<DQK, DO, 8>(a, s);   // 8 waves share each K/V tile
   else if (blocks4 >= 512) launch_t<DQK, DO, 4>(a, s);
   else launch_t<DQK, DO, 2>(a, s);
 }
