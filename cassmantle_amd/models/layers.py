@@ -76,6 +76,11 @@ class StatsArena:
         self.device = x.device
         return self
 
+    def take_rows(self, rows: int) -> Optional[torch.Tensor]:
+        """A zeroed int64 [rows, 2] slice for LayerNorm row statistics (ops.linear row_stats)."""
+        s = self.take(1, rows)
+        return None if s is None else s.view(rows, 2)
+
     def take(self, B: int, C: int) -> Optional[torch.Tensor]:
         if not self.on:
             return None
@@ -98,8 +103,8 @@ class Linear(nn.Module):
         self.weight = _param((fout, fin), std if std is not None else 1.0 / math.sqrt(fin), gen, dtype)
         self.bias = _param((fout,), 0.02, gen, dtype) if bias else None
 
-    def forward(self, x, residual=None, act=None, stats=None):
-        return ops.linear(x, self.weight, self.bias, residual=residual, act=act, stats=stats)
+    def forward(self, x, residual=None, act=None, stats=None, row_stats=None):
+        return ops.linear(x, self.weight, self.bias, residual=residual, act=act, stats=stats, row_stats=row_stats)
 
 
 class Conv2d(nn.Module):
@@ -199,9 +204,11 @@ class SelfAttention(nn.Module):
         self.to_qkv = Linear(dim, 3 * dim, bias=qkv_bias, gen=gen, dtype=dtype)
         self.to_out = Linear(dim, dim, bias=out_bias, gen=gen, dtype=dtype)
 
-    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False, qkv=None, kv8=None):
+    def forward(self, x, residual=None, causal=False, kv_lens=None, fp8=False, qkv=None, kv8=None,
+                row_stats=None):
         """``qkv``: the fused projection already computed (e.g. with a folded LayerNorm);
-        ``kv8``: its K/V as the fp8 attention image (ops.ln_linear(kv8=...)), fp8 only."""
+        ``kv8``: its K/V as the fp8 attention image (ops.ln_linear(kv8=...)), fp8 only;
+        ``row_stats``: LayerNorm row statistics of the output for the next folded projection."""
         if qkv is None:
             qkv = self.to_qkv(x)
         B, N = qkv.shape[0], qkv.shape[1]
@@ -212,7 +219,7 @@ class SelfAttention(nn.Module):
             o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, fp8=True, kv8=kv8)
         else:
             o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=causal, kv_lens=kv_lens, fp8=fp8)
-        return self.to_out(o.reshape(B, N, C), residual=residual)
+        return self.to_out(o.reshape(B, N, C), residual=residual, row_stats=row_stats)
 
 
 class CrossAttention(nn.Module):
@@ -227,8 +234,9 @@ class CrossAttention(nn.Module):
     _kv = None   # view into the UNet's batched context-K/V buffer (set by UNet.set_context)
     _kv8 = None  # its OCP-e4m3 image for the fp8 kernel (set by UNet.set_context(fp8=True))
 
-    def forward(self, x, ctx, residual=None, fp8=False, q=None):
-        """``q``: the query projection already computed (e.g. with a folded LayerNorm)."""
+    def forward(self, x, ctx, residual=None, fp8=False, q=None, row_stats=None):
+        """``q``: the query projection already computed (e.g. with a folded LayerNorm);
+        ``row_stats``: LayerNorm row statistics of the output for the next folded projection."""
         if q is None:
             q = self.to_q(x)
         B, N = q.shape[0], q.shape[1]
@@ -244,7 +252,7 @@ class CrossAttention(nn.Module):
         else:
             kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, self.heads, self.head_dim)
         o = ops.attention(q, kv[:, :, 0], kv[:, :, 1], fp8=fp8, kv8=kv8)
-        return self.to_out(o.reshape(B, N, C), residual=residual)
+        return self.to_out(o.reshape(B, N, C), residual=residual, row_stats=row_stats)
 
 
 class GEGLUFeedForward(nn.Module):

@@ -143,14 +143,43 @@ class CLIPTextEncoder(nn.Module):
             pooled = self.text_projection(ops.gather_add(last.reshape(B * L, -1), eos_rows))
         return hidden, pooled
 
-    def encode(self, texts: Sequence[str], device, output_hidden: int = -1):
+    def encode(self, texts: Sequence[str], device, output_hidden: int = -1, graphs: bool = False):
+        """Tokenise on the host, encode on ``device``.  ``graphs`` (GPU): the encoder forward is
+        captured once per (batch, output) shape and replayed -- ~12 (CLIP-L) / 32 (bigG) layers
+        of launches per generation become one graph launch; the outputs are copied out of the
+        graph's static buffers, so they outlive the next call."""
         ids, _ = self.tokenizer(texts, pad_to=self.cfg.max_positions)
         eos_rows = None
         if self.text_projection is not None:
             B, L = ids.shape
-            eos_rows = (torch.arange(B) * L + (ids == self.tokenizer.eos).int().argmax(dim=1)).int().to(device)
-        # int32 ids, converted on the host: the embedding gather takes them as they are
-        return self.forward(ids.int().to(device), output_hidden, eos_rows)
+            eos_rows = (torch.arange(B) * L + (ids == self.tokenizer.eos).int().argmax(dim=1)).int()
+        if not graphs or torch.device(device).type != "cuda" or ops.get_mode() != "hip":
+            # int32 ids, converted on the host: the embedding gather takes them as they are
+            return self.forward(ids.int().to(device), output_hidden,
+                                None if eos_rows is None else eos_rows.to(device))
+        key = (tuple(ids.shape), output_hidden, str(device))
+        g = self.__dict__.setdefault("_graphs", {}).get(key)
+        if g is None:
+            sid = ids.int().to(device)
+            seos = None if eos_rows is None else eos_rows.to(device)
+            s = torch.cuda.Stream(device=device)
+            s.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(s):
+                self.forward(sid, output_hidden, seos)              # warm-up: allocator, GEMM plans
+            torch.cuda.current_stream(device).wait_stream(s)
+            from ..utils.tracing import TRACER
+            graph = torch.cuda.CUDAGraph()
+            with TRACER.capturing(), torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                out = self.forward(sid, output_hidden, seos)
+            g = self._graphs[key] = (graph, sid, seos, out)
+        graph, sid, seos, (hidden, pooled) = g
+        sid.copy_(ids.int())
+        if seos is not None:
+            seos.copy_(eos_rows)
+        graph.replay()
+        h = ops.copy_(torch.empty_like(hidden), hidden)
+        p = None if pooled is None else ops.copy_(torch.empty_like(pooled), pooled)
+        return h, p
 
 
 @dataclass

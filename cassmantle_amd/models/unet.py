@@ -108,6 +108,21 @@ class ResnetBlock(nn.Module):
 # other K take a read-only row-statistics pass + epilogue correction.  On by default;
 # CASSMANTLE_LN_FOLD=0 restores LayerNorm kernel + plain GEMM.
 _LN_FOLD = os.environ.get("CASSMANTLE_LN_FOLD", "1") == "1"
+# LayerNorm row statistics from the producing GEMM epilogues where the folded projection could not
+# compute them itself (C other than 320 / 640: the SD-1.5 16^2 / 8^2 levels, every SDXL
+# transformer level above 64^2): no row-statistics kernel per LayerNorm.  CASSMANTLE_LN_ROWSTATS=0
+# restores the statistics pass (A/B knob)
+_LN_ROWSTATS = os.environ.get("CASSMANTLE_LN_ROWSTATS", "1") == "1"
+# transformer GroupNorm folded into proj_in where the A-in-registers kernel takes it (C = 320 /
+# 640): verdict r2 item 1c.  CASSMANTLE_GN_FOLD=0 restores GroupNorm apply + GEMM (A/B knob)
+_GN_FOLD = os.environ.get("CASSMANTLE_GN_FOLD", "1") == "1"
+
+
+def _row_stats_wanted(x: torch.Tensor) -> bool:
+    return (_LN_ROWSTATS and x.device.type == "cuda" and ops.get_mode() == "hip" and ops.LN_FOLD_MODE == 1
+            and x.shape[-1] not in (320, 640) and x.shape[-1] % 8 == 0 and x.numel() // x.shape[-1] > 8)
+
+
 # fp8 self-attention K/V emitted by the QKV projection's epilogue (no per-call pack kernel);
 # CASSMANTLE_FP8_KV_EPILOGUE=0 restores the pack (A/B knob)
 _FP8_KV_EPILOGUE = os.environ.get("CASSMANTLE_FP8_KV_EPILOGUE", "1") == "1"
@@ -143,26 +158,37 @@ class BasicTransformerBlock(nn.Module):
         return tuple((self._buffers[f"fold{i}_w"], self._buffers[f"fold{i}_s"], self._buffers[f"fold{i}_b"])
                      for i in range(3))
 
-    def forward(self, x, ctx, fp8=False):
+    def forward(self, x, ctx, fp8=False, arena: Optional[StatsArena] = None, xrs=None):
+        """``arena`` / ``xrs``: where the folded LayerNorms need row statistics (C not taken by the
+        A-in-registers kernel, see :func:`_row_stats_wanted`), each producer of a LayerNorm input --
+        the previous block or proj_in (``xrs``), the two attention output projections -- accumulates
+        them in its epilogue into an arena slice; the folded projection reads them (no row-stats
+        pass).  Returns (x, row statistics of x or None)."""
         if _LN_FOLD and x.device.type == "cuda" and ops.get_mode() == "hip":
-            # the three LayerNorms are folded into the projections that consume them: a
-            # read-only row-statistics pass each, no normalised activation in HBM
+            # the three LayerNorms are folded into the projections that consume them: no
+            # normalised activation in HBM
             f = self.folds()
             n1, n2, n3 = self.norm1, self.norm2, self.norm3
+            want = arena is not None and _row_stats_wanted(x)
+            rows = x.numel() // x.shape[-1]
             # fp8 (SDXL): the QKV epilogue writes K/V straight into the fp8 attention image
             kv8 = None
             if fp8 and _FP8_KV_EPILOGUE and ops.kv8_ok(x, self.attn1.head_dim):
                 kv8 = ops.kv8_image(x.shape[0], x.shape[1], x.shape[2], x.device)
-            qkv = ops.ln_linear(x, n1.weight, n1.bias, n1.eps, self.attn1.to_qkv.weight, fold=f[0], kv8=kv8)
-            x = self.attn1(None, residual=x, fp8=fp8, qkv=qkv, kv8=kv8)
-            q = ops.ln_linear(x, n2.weight, n2.bias, n2.eps, self.attn2.to_q.weight, fold=f[1])
-            x = self.attn2(None, ctx, residual=x, fp8=fp8, q=q)
-            h = ops.ln_linear(x, n3.weight, n3.bias, n3.eps, self.ff.proj_in.weight, act="geglu", fold=f[2])
-            return self.ff.proj_out(h, residual=x)
+            qkv = ops.ln_linear(x, n1.weight, n1.bias, n1.eps, self.attn1.to_qkv.weight, fold=f[0], kv8=kv8,
+                                row_stats=xrs if want else None)
+            r2 = arena.take_rows(rows) if want else None
+            x = self.attn1(None, residual=x, fp8=fp8, qkv=qkv, kv8=kv8, row_stats=r2)
+            q = ops.ln_linear(x, n2.weight, n2.bias, n2.eps, self.attn2.to_q.weight, fold=f[1], row_stats=r2)
+            r3 = arena.take_rows(rows) if want else None
+            x = self.attn2(None, ctx, residual=x, fp8=fp8, q=q, row_stats=r3)
+            h = ops.ln_linear(x, n3.weight, n3.bias, n3.eps, self.ff.proj_in.weight, act="geglu", fold=f[2],
+                              row_stats=r3)
+            return self.ff.proj_out(h, residual=x), None
         x = self.attn1(self.norm1(x), residual=x, fp8=fp8)
         x = self.attn2(self.norm2(x), ctx, residual=x, fp8=fp8)
         x = self.ff(self.norm3(x), residual=x)
-        return x
+        return x, None
 
 
 class Transformer2D(nn.Module):
@@ -176,10 +202,21 @@ class Transformer2D(nn.Module):
 
     def forward(self, x, ctx, fp8=False, arena: Optional[StatsArena] = None, xs=None):
         B, H, W, C = x.shape
-        h = self.norm(x, stats=xs).view(B, H * W, C)
-        h = self.proj_in(h)
-        for blk in self.transformer_blocks:
-            h = blk(h, ctx, fp8=fp8)
+        hrs = None
+        if (_GN_FOLD and xs is not None and C in (320, 640) and (H * W) % 256 == 0 and x.device.type == "cuda"
+                and ops.get_mode() == "hip"):
+            # GroupNorm folded into proj_in (A-in-registers GEMM): no GroupNorm pass over x
+            n = self.norm
+            h = ops.gn_linear(x.view(B, H * W, C), xs, n.weight, n.bias, n.groups, n.eps, self.proj_in.weight,
+                              self.proj_in.bias)
+        else:
+            h = self.norm(x, stats=xs).view(B, H * W, C)
+            # row statistics of proj_in's output for the first block's folded LayerNorm (later
+            # blocks' inputs come from a split-K feed-forward GEMM: they keep the statistics pass)
+            hrs = arena.take_rows(B * H * W) if (arena is not None and _LN_FOLD and _row_stats_wanted(h)) else None
+            h = self.proj_in(h, row_stats=hrs)
+        for i, blk in enumerate(self.transformer_blocks):
+            h, _ = blk(h, ctx, fp8=fp8, arena=arena, xrs=hrs if i == 0 else None)
         so = arena.take(B, C) if arena is not None else None
         return self.proj_out(h, residual=x.view(B, H * W, C), stats=so).view(B, H, W, C), so
 

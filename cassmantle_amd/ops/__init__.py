@@ -88,12 +88,12 @@ def record_gemms(on: bool) -> Optional[list]:
     return rec
 
 
-def _launch(fn, *args):
+def _launch(fn, *args, **kw):
     if not _tune_loaded:
         load_gemm_tuning()
-    fn(*args)
+    fn(*args, **kw)
     if _RECORD is not None:
-        _RECORD.append((ext().gemm_last_key(), lambda: fn(*args)))
+        _RECORD.append((ext().gemm_last_key(), lambda: fn(*args, **kw)))
 
 
 _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5, "swiglu": 6}
@@ -135,13 +135,17 @@ def channel_stats(y: torch.Tensor, stats: torch.Tensor) -> None:
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: Optional[str] = None,
-           stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           row_stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(x @ w^T + bias) + residual.  x [..., K], w [N, K] (or [2N, K] for geglu).
     ``out``: a contiguous [..., N] buffer of x's dtype to write y into (else a new tensor).
 
     ``stats`` (:func:`new_stats` [B, N, 2], zeroed; B = x.shape[0]): per-(image, channel) sum and
     sum-of-squares of y are accumulated into it by the GEMM epilogue, for a following
-    :func:`group_norm` (no statistics pass over y)."""
+    :func:`group_norm` (no statistics pass over y).
+    ``row_stats`` (zeroed int64 [rows, 2], HIP path only): per-row fixed-point sum and
+    sum-of-squares of y, for a following LayerNorm-folded :func:`ln_linear` (``row_stats=``
+    there): the consumer then needs no row-statistics pass."""
     if not _use_hip(x):
         if x.device.type == "cuda":  # explicit torch baseline mode: stock ops in bf16
             y = _torch_linear(x, w, bias, residual, act)
@@ -162,8 +166,35 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     o2 = out.view(x2.shape[0], N)
     r2 = residual.reshape(-1, N) if residual is not None else None
     hw = x2.shape[0] // x.shape[0] if stats is not None else 0
-    _launch(ext().gemm, x2, w, bias, r2, o2, _ACT[act], stats, hw)
+    if row_stats is not None:
+        _launch(ext().gemm, x2, w, bias, r2, o2, _ACT[act], stats, hw, row_stats=row_stats)
+    else:
+        _launch(ext().gemm, x2, w, bias, r2, o2, _ACT[act], stats, hw)
     return out.view(*x.shape[:-1], N)
+
+
+def gn_linear(x: torch.Tensor, stats: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int,
+              eps: float, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+              residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear(group_norm(x), w, bias, residual)`` for x [B, S, C] with the producer statistics
+    ``stats`` of x (int64 [B, C, 2], see :func:`new_stats`; no SiLU: the transformer GroupNorm ->
+    proj_in).  On the HIP path the A-in-registers GEMM applies the GroupNorm to its resident A rows
+    (C = 320 / 640, images of a multiple of 256 rows): no GroupNorm kernel, no normalised copy
+    of x in HBM; other shapes run the statistics-driven GroupNorm apply, then the GEMM."""
+    B, C = x.shape[0], x.shape[-1]
+    if not _use_hip(x):
+        xn = group_norm(x, groups, gamma, beta, eps, False, stats=stats)
+        return linear(xn, w, bias, residual=residual)
+    rows = x.numel() // C
+    x2 = x.reshape(rows, C)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    N = w.shape[0]
+    out = torch.empty((rows, N), device=x.device, dtype=x.dtype)
+    r2 = residual.reshape(rows, N) if residual is not None else None
+    _launch(ext().gemm, x2, w, bias, r2, out, 0, None, 0, gn_stats=stats, gn_gamma=gamma, gn_beta=beta,
+            gn_groups=int(groups), gn_hw=rows // B, gn_eps=float(eps))
+    return out.reshape(*x.shape[:-1], N)
 
 
 def ln_fold(ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], w: torch.Tensor,
@@ -202,7 +233,8 @@ LN_FOLD_MODE = int(os.environ.get("CASSMANTLE_LN_FOLD_MODE", "1"))
 
 def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.Tensor], eps: float,
               w: torch.Tensor, bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
-              act: Optional[str] = None, fold=None, kv8: Optional[torch.Tensor] = None) -> torch.Tensor:
+              act: Optional[str] = None, fold=None, kv8: Optional[torch.Tensor] = None,
+              row_stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``linear(layer_norm(x), w, bias, residual, act)``.  With ``fold`` (:func:`ln_fold` of these
     weights) on the HIP path the LayerNorm is folded into the GEMM: a read-only row-statistics
     pass, then the GEMM on the raw rows with the folded weights and a per-row epilogue
@@ -211,7 +243,10 @@ def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.
     ``kv8`` (x [B, N, C] -> fused Q|K|V [B, N, 3C] of 64-wide heads, N % 64 == 0): the epilogue
     writes the K and V columns as the e4m3 image of the fp8 attention kernel (:func:`kv8_image`)
     into ``kv8`` instead of bf16 (those columns of the result are then undefined): self-attention
-    needs no per-call pack."""
+    needs no per-call pack.
+
+    ``row_stats``: the row statistics of x that x's producer accumulated (:func:`linear`
+    ``row_stats=``): the GEMM epilogue derives mean / rstd from them, no statistics pass."""
     K = x.shape[-1]
     rows = x.numel() // K
     if fold is None or not _use_hip(x) or rows <= 8 or K % 8 or (LN_FOLD_MODE == 2 and K not in (320, 640)):
@@ -228,10 +263,13 @@ def ln_linear(x: torch.Tensor, ln_weight: torch.Tensor, ln_bias: Optional[torch.
     r2 = residual.reshape(rows, N) if residual is not None else None
     # row statistics: inside the A-in-registers GEMM when it takes the shape (K = 320 / 640),
     # else one read-only stats pass chosen by the binding
+    fx = {"ln_rows_fx": row_stats} if row_stats is not None else {}
     if kv8 is not None:
         C = N // 3
         _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps), kv8, C,
-                int(x.shape[-2]), C // 64)
+                int(x.shape[-2]), C // 64, **fx)
+    elif fx:
+        _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps), **fx)
     else:
         _launch(ext().gemm, x2, wf, bf, r2, out, _ACT[act], None, 0, None, wsum, float(eps))
     return out.reshape(*x.shape[:-1], N)

@@ -69,7 +69,10 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
           const c10::optional<at::Tensor>& residual, at::Tensor& out, int64_t act,
           const c10::optional<at::Tensor>& stats, int64_t stats_hw,
           const c10::optional<at::Tensor>& ln_rows, const c10::optional<at::Tensor>& ln_wsum, double ln_eps,
-          const c10::optional<at::Tensor>& kv8, int64_t kv8_col0, int64_t kv8_ntok, int64_t kv8_hk) {
+          const c10::optional<at::Tensor>& kv8, int64_t kv8_col0, int64_t kv8_ntok, int64_t kv8_hk,
+          const c10::optional<at::Tensor>& ln_rows_fx, const c10::optional<at::Tensor>& row_stats,
+          const c10::optional<at::Tensor>& gn_stats, const c10::optional<at::Tensor>& gn_gamma,
+          const c10::optional<at::Tensor>& gn_beta, int64_t gn_groups, int64_t gn_hw, double gn_eps) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK(x.stride(1) == 1, "gemm: x rows must be contiguous");
@@ -106,6 +109,61 @@ void gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     TORCH_CHECK(stats_hw > 0 && p.M % stats_hw == 0, "gemm: stats_hw must divide the rows");
     p.stats_hw = (int)stats_hw;
     p.stats = opt_stats(stats, p.M / stats_hw, p.N);
+  }
+  if (gn_stats.has_value() && gn_stats->defined()) {
+    // GroupNorm (no SiLU) of x folded into the A-in-registers GEMM (transformer GroupNorm ->
+    // proj_in); shapes that kernel does not take run the stats-driven GroupNorm apply + GEMM
+    TORCH_CHECK(gn_gamma.has_value() && gn_beta.has_value() && gn_groups > 0 && gn_hw > 0 && p.M % gn_hw == 0,
+                "gemm: gn_stats needs gamma, beta, groups and rows per image");
+    CHECK_DEV(*gn_stats); CHECK_CONTIG(*gn_stats);
+    TORCH_CHECK(gn_stats->scalar_type() == at::kLong && gn_stats->numel() == 2LL * (p.M / gn_hw) * p.K,
+                "gemm: gn_stats int64 [images, K, 2]");
+    TORCH_CHECK(!(ln_wsum.has_value() && ln_wsum->defined()) && !(row_stats.has_value() && row_stats->defined()) &&
+                    !(kv8.has_value() && kv8->defined()) && !(stats.has_value() && stats->defined()),
+                "gemm: gn_stats excludes LayerNorm folds, row / GroupNorm output statistics and kv8");
+    p.gn_stats = reinterpret_cast<const long long*>(gn_stats->data_ptr<int64_t>());
+    p.gn_gamma = opt_bptr(gn_gamma);
+    p.gn_beta = opt_bptr(gn_beta);
+    p.gn_groups = (int)gn_groups;
+    p.gn_hw = (int)gn_hw;
+    p.gn_eps = (float)gn_eps;
+    if (gemm_areg_ok(p)) {
+      run_gemm(p, out);                           // the planner maps gn_stats to the A-in-registers kernel
+      return;
+    }
+    TORCH_CHECK(x.is_contiguous() && p.K % 8 == 0 && p.K % gn_groups == 0, "gemm gn fallback: contiguous rows");
+    at::Tensor xn = at::empty_like(x);
+    launch_group_norm_cs(bptr(x), nullptr, p.gn_stats, p.K, nullptr, p.gn_gamma, p.gn_beta, bptr_mut(xn),
+                         p.M / gn_hw, gn_hw, p.K, (int)gn_groups, (float)gn_eps, 0, cur_stream());
+    p.gn_stats = nullptr; p.gn_gamma = nullptr; p.gn_beta = nullptr;
+    p.A = bptr(xn);
+    run_gemm(p, out);
+    return;
+  }
+  if (row_stats.has_value() && row_stats->defined()) {
+    // LayerNorm row statistics of this output for a folded consumer (the LDS-staged epilogue
+    // accumulates them; the planner then never splits K)
+    CHECK_DEV(*row_stats); CHECK_CONTIG(*row_stats);
+    TORCH_CHECK(row_stats->scalar_type() == at::kLong && row_stats->numel() == 2LL * p.M,
+                "gemm: row_stats zeroed int64 [M, 2]");
+    TORCH_CHECK(p.stats == nullptr && p.kv8 == nullptr && !p.out_f32 && p.batch == 1 && p.M > 8 && p.N % 8 == 0 &&
+                    p.ldc % 8 == 0 && p.K % 8 == 0 && p.lda % 8 == 0,
+                "gemm: row_stats needs the LDS-staged bf16 epilogue (no GroupNorm stats / kv8, N % 8 == 0, M > 8)");
+    p.row_stats = reinterpret_cast<long long*>(row_stats->data_ptr<int64_t>());
+  }
+  if (ln_rows_fx.has_value() && ln_rows_fx->defined()) {
+    // folded LayerNorm on row statistics a producer epilogue accumulated (no statistics pass)
+    TORCH_CHECK(ln_wsum.has_value() && ln_wsum->defined() && ln_eps > 0 && !(ln_rows.has_value() && ln_rows->defined()),
+                "gemm: ln_rows_fx needs ln_wsum and ln_eps, and excludes ln_rows");
+    CHECK_DEV(*ln_rows_fx); CHECK_CONTIG(*ln_rows_fx); CHECK_DEV(*ln_wsum); CHECK_CONTIG(*ln_wsum);
+    TORCH_CHECK(ln_rows_fx->scalar_type() == at::kLong && ln_rows_fx->numel() == 2LL * p.M, "gemm: ln_rows_fx int64 [M, 2]");
+    TORCH_CHECK(ln_wsum->scalar_type() == at::kFloat && ln_wsum->numel() == p.Nw, "gemm: ln_wsum fp32 [Nw]");
+    TORCH_CHECK(p.M > 8 && p.K % 8 == 0 && p.lda % 8 == 0 && !p.out_f32, "gemm: folded LayerNorm needs the MFMA path");
+    p.ln_rows_fx = reinterpret_cast<const long long*>(ln_rows_fx->data_ptr<int64_t>());
+    p.ln_wsum = ln_wsum->data_ptr<float>();
+    p.ln_eps = (float)ln_eps;
+    run_gemm(p, out);
+    return;
   }
   if (ln_rows.has_value() && ln_rows->defined()) {
     // folded LayerNorm: raw rows in, per-row (mean, rstd) + column sums of the folded weights
@@ -733,7 +791,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("out"),
         py::arg("act"), py::arg("stats"), py::arg("stats_hw"), py::arg("ln_rows") = py::none(),
         py::arg("ln_wsum") = py::none(), py::arg("ln_eps") = 0.0, py::arg("kv8") = py::none(),
-        py::arg("kv8_col0") = 0, py::arg("kv8_ntok") = 0, py::arg("kv8_hk") = 0, nogil());
+        py::arg("kv8_col0") = 0, py::arg("kv8_ntok") = 0, py::arg("kv8_hk") = 0, py::arg("ln_rows_fx") = py::none(),
+        py::arg("row_stats") = py::none(), py::arg("gn_stats") = py::none(), py::arg("gn_gamma") = py::none(),
+        py::arg("gn_beta") = py::none(), py::arg("gn_groups") = 0, py::arg("gn_hw") = 0, py::arg("gn_eps") = 0.0, nogil());
   m.def("row_stats", &row_stats, nogil());
   m.def("gemm_cat", &gemm_cat, nogil());
   m.def("group_norm_cat", &group_norm_cat, nogil());

@@ -159,7 +159,8 @@ std::string gemm_key(const GemmArgs& p) {
   snprintf(buf, sizeof(buf), "m%d n%d k%d w%d b%d c%d:%d:%d:%d:%d:%d:%d:%d p%d a%d g%d s%d r%d cb%d ln%d f%d",
            p.M, p.N, p.K, p.Nw, p.batch, p.conv, p.IH, p.IW, p.Cin, p.stride, p.ksize, p.pad, p.upsample, p.parity,
            p.A2 != nullptr, is_gated(p.act) ? 1 : 0, p.stats != nullptr, p.residual != nullptr, p.chan_bias != nullptr,
-           p.ln_rows != nullptr ? 1 : (p.ln_wsum != nullptr ? 2 : 0), p.out_f32);
+           (p.ln_rows != nullptr || p.ln_rows_fx != nullptr) ? 1 : (p.ln_wsum != nullptr ? 2 : (p.gn_stats ? 3 : 0)),
+           p.out_f32);
   return std::string(buf);
 }
 
@@ -198,7 +199,13 @@ void gemm_set_override(int cfg, int split) {
 
 static GemmPlan gemm_plan_impl(const GemmArgs& p);
 GemmPlan gemm_plan(const GemmArgs& p) {
-  const GemmPlan r = gemm_plan_impl(p);
+  GemmPlan r = gemm_plan_impl(p);
+  if (p.row_stats != nullptr) {
+    // output row statistics exist only in the shared LDS-staged epilogue (tile_epilogue):
+    // no split-K, not the A-in-registers kernel
+    if (r.cfg == kAreg) r.cfg = 3;
+    r.split = 1;
+  }
   g_last_plan = r;
   return r;
 }
@@ -218,7 +225,10 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   if (g_record_key) g_last_key = gemm_key(p);
   // in-kernel LayerNorm statistics exist only in the A-in-registers kernel (the binding checked
   // eligibility, so neither the table nor a forced config may pick anything else)
-  if (p.ln_wsum != nullptr && p.ln_rows == nullptr) return GemmPlan{kAreg, 1};
+  if (p.ln_wsum != nullptr && p.ln_rows == nullptr && p.ln_rows_fx == nullptr) return GemmPlan{kAreg, 1};
+  // GroupNorm folded into the A rows: only the A-in-registers kernel applies it (the binding
+  // checked eligibility)
+  if (p.gn_stats != nullptr) return GemmPlan{kAreg, 1};
   if (force_cfg < 0) {
     bool have = false;
     GemmPlan tp{0, 1};

@@ -90,7 +90,8 @@ constexpr int areg_minb() {
 // bias = bias + W . beta folded offline): row statistics from the fragments, then every
 // fragment is normalised in place to bf16 -- exactly the LayerNorm kernel's output, with no
 // LayerNorm kernel, no normalised copy in HBM, no stats pass, and a plain epilogue
-template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
+// GNK: GroupNorm (p.gn_stats) applied to the resident A rows, see the prologue below
+template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK, bool GNK = false>
 __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_areg_kernel(GemmArgs p, int chunks_per_block) {
   constexpr int AR_BM = 64 * RW;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -181,6 +182,74 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
     // The opaque asm below makes the normalised fragments inputs of a memory-clobbering
     // statement, so no DMA can be scheduled above the statistics.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        i32x4_t t = __builtin_bit_cast(i32x4_t, afr[j][ks]);
+        asm volatile("" : "+v"(t) : : "memory");
+        afr[j][ks] = __builtin_bit_cast(bf16x8_t, t);
+      }
+  }
+
+  // ---- GroupNorm of the A rows (p.gn_stats; transformer GroupNorm -> proj_in, no SiLU): the
+  // block's rows lie in one image (host: gn_hw % (64 RW) == 0).  Fold the image's K channel
+  // (sum, sum of squares) into per-group (mean, rstd) in LDS (8 threads per group), then scale /
+  // shift every resident fragment in place.  Scalar fp32 and finished before the first DMA, as
+  // the LayerNorm prologue above (race note at sum_row_groups); the LDS scratch is released by
+  // a barrier before the ring is staged.
+  if constexpr (GNK) {
+    float* gs = reinterpret_cast<float*>(smem);            // [G][2] mean, rstd
+    const int G = p.gn_groups;
+    constexpr int K = 32 * KS;
+    const int img = (blockIdx.x * AR_BM) / p.gn_hw;
+    const long long* st = p.gn_stats + (long long)img * K * 2;
+    const int Cg = K / G;
+    for (int g0 = 0; g0 < G; g0 += AR_THREADS / 8) {
+      const int g = g0 + tid / 8, sub = tid % 8;
+      long long si = 0, qi = 0;
+      if (g < G)
+        for (int c = g * Cg + sub; c < (g + 1) * Cg; c += 8) {
+          si += st[2 * c];
+          qi += st[2 * c + 1];
+        }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        si += __shfl_xor(si, o, 64);
+        qi += __shfl_xor(qi, o, 64);
+      }
+      if (g < G && sub == 0) {
+        const double n = (double)p.gn_hw * Cg;
+        const double mean = stat_decode(si, 0) / n;
+        double var = stat_decode(qi, 1) / n - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        gs[2 * g] = (float)mean;
+        gs[2 * g + 1] = (float)(1.0 / sqrt(var + (double)p.gn_eps));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = 32 * ks + 8 * fq;                     // this lane's 8 channels of k-step ks
+      float ga[8], be[8], sc[8], sh[8];
+      unpack8(*reinterpret_cast<const uint4*>(p.gn_gamma + c0), ga);
+      unpack8(*reinterpret_cast<const uint4*>(p.gn_beta + c0), be);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = ((c0 + e) * G) / K;                   // K is a compile-time constant
+        sc[e] = scalar_f(ga[e] * gs[2 * g + 1]);
+        sh[e] = scalar_f(be[e] - scalar_f(gs[2 * g] * sc[e]));
+      }
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        float f[8];
+        unpack8(__builtin_bit_cast(uint4, afr[j][ks]), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = scalar_f(fmaf(f[e], sc[e], sh[e]));
+        afr[j][ks] = as_bf16x8(pack8(f));
+      }
+    }
+    __syncthreads();                                       // gs consumed: the ring may overwrite it
 #pragma unroll
     for (int j = 0; j < RW; ++j)
 #pragma unroll
@@ -375,7 +444,7 @@ __global__ void __launch_bounds__(AR_THREADS, (areg_minb<KS, TI, RING>())) gemm_
   areg_wait_vmcnt<0>();
 }
 
-template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK>
+template <int KS, int TI, int RING, int RW, bool GEGLU, bool LNK, bool GNK = false>
 void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   constexpr int AR_BM = 64 * RW;
   constexpr int BNC = 16 * TI;
@@ -389,7 +458,7 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
   const int per = (nchunks + groups - 1) / groups;
   groups = (nchunks + per - 1) / per;   // no block without chunks
   const size_t lds = (size_t)RING * BNC * (KS / 2) * 128;
-  auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU, LNK>;
+  auto* kfn = &gemm_areg_kernel<KS, TI, RING, RW, GEGLU, LNK, GNK>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -404,6 +473,15 @@ void launch_areg_t(const GemmArgs& p, hipStream_t s) {
 // K = 320: 64-row chunks, 3-deep ring (120 KiB); K = 640: 32-row chunks, 3-deep ring (120 KiB)
 bool gemm_areg_ok(const GemmArgs& p) {
   if (p.conv || p.A2 || p.batch != 1 || p.out_f32 || p.ln_rows || p.chan_bias || p.split > 1) return false;
+  if (p.ln_rows_fx != nullptr || p.row_stats != nullptr) return false;
+  if (p.gn_stats != nullptr) {
+    // GroupNorm fold: K = 320 / 640 tiles (not the K = 1280 variant), no LayerNorm, every
+    // block's rows in one image (64 RW <= 256 rows), 8-channel vectors inside the groups
+    if (p.ln_wsum || is_gated(p.act) || !(p.K == 320 || p.K == 640) || p.gn_hw <= 0 || p.gn_hw % 256 ||
+        p.M % p.gn_hw)
+      return false;
+    if (p.gn_groups <= 0 || p.K % p.gn_groups || p.gn_gamma == nullptr || p.gn_beta == nullptr) return false;
+  }
   if (p.ln_wsum && !(p.ln_eps > 0.f)) return false;
   // K = 1280 (16 rows per wave, 160 A registers, 16-row W chunks on a 2-deep ring): the
   // latency-bound level-3 projections (M = 2048); opt-in while it is being measured
@@ -468,6 +546,12 @@ void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
 }
 
 void launch_gemm_areg(const GemmArgs& p, hipStream_t s) {
+  if (p.gn_stats != nullptr) {
+    // GroupNorm-folded proj_in (non-gated, K = 320 / 640): the default tiles of those shapes
+    if (p.K == 320) launch_areg_t<10, 2, 3, 2, false, false, true>(p, s);
+    else launch_areg_t<20, 2, 2, 2, false, false, true>(p, s);
+    return;
+  }
   if (p.ln_wsum != nullptr) launch_gemm_areg_t<true>(p, s);
   else launch_gemm_areg_t<false>(p, s);
 }

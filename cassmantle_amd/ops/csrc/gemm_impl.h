@@ -67,9 +67,21 @@ CM_DEVICE void add4(float* o, uint2 v) {
   o[0] += bf2f(v.x & 0xffff); o[1] += bf2f(v.x >> 16); o[2] += bf2f(v.y & 0xffff); o[3] += bf2f(v.y >> 16);
 }
 
-// folded LayerNorm (p.ln_rows): o = rstd_m * (acc - mean_m * wsum[n..n+3]) for the W rows n..n+3
+// folded LayerNorm (p.ln_rows, or p.ln_rows_fx from a producer epilogue): o = rstd_m * (acc -
+// mean_m * wsum[n..n+3]) for the W rows n..n+3
+CM_DEVICE float2 ln_row(const GemmArgs& p, int m) {
+  if (p.ln_rows_fx != nullptr) {
+    const longlong2 v = reinterpret_cast<const longlong2*>(p.ln_rows_fx)[m];
+    const double inv = 1.0 / p.K;
+    const double mean = (double)v.x * (inv / STAT_SCALE_SUM);
+    double var = (double)v.y * (inv / STAT_SCALE_SQ) - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    return make_float2((float)mean, rsqrtf((float)var + p.ln_eps));
+  }
+  return reinterpret_cast<const float2*>(p.ln_rows)[m];
+}
 CM_DEVICE void ln_fold4(const GemmArgs& p, int m, int wn, float* o) {
-  const float2 ms = reinterpret_cast<const float2*>(p.ln_rows)[m];
+  const float2 ms = ln_row(p, m);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, p.ln_wsum[wn + r], o[r]);
 }
@@ -94,7 +106,7 @@ CM_DEVICE void epilogue4(const GemmArgs& p, int batch, int m, int n, float* o) {
   const long long cbs = p.ldcb ? p.ldcb : p.N;
   const bool full = (n + 4 <= p.N) && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (cbs % 4 == 0);
   const long long om = out_row(p, m, batch);
-  if (p.ln_rows) ln_fold4(p, m, n, o);
+  if (p.ln_rows || p.ln_rows_fx) ln_fold4(p, m, n, o);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
   if (full) {
@@ -142,7 +154,7 @@ CM_DEVICE void epilogue4_call(const GemmArgs& p, int batch, int m, int n, f32x4_
 
 CM_DEVICE void gated_epilogue4_call(const GemmArgs& p, int batch, int m, int n, f32x4_t hv, f32x4_t gv) {
   float o[4], hh[4] = {hv[0], hv[1], hv[2], hv[3]}, gg[4] = {gv[0], gv[1], gv[2], gv[3]};
-  if (p.ln_rows) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
+  if (p.ln_rows || p.ln_rows_fx) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float h = hh[r], g = gg[r];
@@ -192,7 +204,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
             float o[4], hh[4], gg[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
-            if (p.ln_rows && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
+            if ((p.ln_rows || p.ln_rows_fx) && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float h = hh[r], g = gg[r];
@@ -207,7 +219,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
             const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
             const int n = n0 + nl;
             float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (p.ln_rows && n < p.N && m < p.M) ln_fold4(p, m, n, o);
+            if ((p.ln_rows || p.ln_rows_fx) && n < p.N && m < p.M) ln_fold4(p, m, n, o);
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
             if (n < p.N && m < p.M) {
@@ -256,7 +268,26 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         for (int c = tid; c < BM * CPR; c += THREADS) {
           const int row = c / CPR, c8 = c - row * CPR;
           if (m0 + row >= p.M || n0 + c8 * 8 >= p.N) continue;
-          finish(row, c8);
+          const uint4 v = finish(row, c8);
+          if (p.row_stats != nullptr) *reinterpret_cast<uint4*>(T + row * OST + c8 * 8) = v;   // stored values
+        }
+        if (p.row_stats != nullptr) {
+          // LayerNorm row statistics of the stored tile for a folded consumer (p.ln_rows_fx there):
+          // one thread per row sums its OBN stored values, one fixed-point atomic pair per row
+          __syncthreads();
+          for (int row = tid; row < BM; row += THREADS) {
+            const int m = m0 + row;
+            if (m >= p.M) break;
+            float sm = 0.f, sq = 0.f;
+            for (int c8 = 0; c8 < CPR && n0 + c8 * 8 < p.N; ++c8) {
+              float f[8];
+              unpack8(*reinterpret_cast<const uint4*>(T + row * OST + c8 * 8), f);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) { sm += f[e]; sq = fmaf(f[e], f[e], sq); }
+            }
+            stat_atomic_add(p.row_stats + 2LL * m, 0, sm);
+            stat_atomic_add(p.row_stats + 2LL * m + 1, 1, sq);
+          }
         }
         if (p.kv8 != nullptr && n0 + OBN > p.kv8_col0 + 64 * p.kv8_hk) {
           // V columns -> V8t rows: d-row of a 64-key block = 64 slot-ordered bytes, written as

@@ -42,6 +42,23 @@ struct GemmArgs {
   // ln_wsum set, ln_rows null, ln_eps > 0: the row statistics are computed INSIDE the kernel from
   // the register-resident A rows (A-in-registers short-K GEMM, gemm_areg.hip, only)
   float ln_eps = 0.f;
+  // folded LayerNorm whose row statistics a PRODUCER epilogue accumulated (row_stats below):
+  // [M][2] int64 fixed-point (sum, sum of squares) over the K columns; mean / rstd (with ln_eps)
+  // are derived in this GEMM's epilogue -- no row-statistics pass
+  const long long* ln_rows_fx = nullptr;
+  // row statistics of THIS GEMM's stored output (after bias / residual), for a LayerNorm-folded
+  // consumer: atomically accumulated [M][2] int64 fixed-point (sum, sum of squares) over the N
+  // columns (zeroed by the caller); LDS-staged bf16 epilogue only (no split-K, no GroupNorm stats)
+  long long* row_stats = nullptr;
+  // GroupNorm (no SiLU) of the A rows folded into the A-in-registers kernel (gemm_areg.hip only):
+  // A = the raw input x, gn_stats = its producer-accumulated per-(image, channel) int64 (sum,
+  // sum of squares) [M / gn_hw][K][2]; the kernel folds them to per-group mean / rstd and applies
+  // x * gamma * rstd + (beta - mean * gamma * rstd) to the register-resident fragments
+  const long long* gn_stats = nullptr;
+  const uint16_t* gn_gamma = nullptr;
+  const uint16_t* gn_beta = nullptr;
+  int gn_groups = 0, gn_hw = 0;
+  float gn_eps = 0.f;
   // GroupNorm statistics of the output: atomically accumulated per-(image, column) sum and
   // sum-of-squares [M / stats_hw][N][2] int64 fixed point (common.h; zeroed by the caller);
   // stats_hw = rows per image

@@ -60,6 +60,9 @@ def default_device() -> torch.device:
 # decode (13.5 vs 11.1 ms per 4-image decode, 558-560 vs 557-558 ms/step, same box x2,
 # profiles/r3_vae_graph_ab.txt); CASSMANTLE_VAE_GRAPH=1 turns it on
 _VAE_GRAPH = os.environ.get("CASSMANTLE_VAE_GRAPH", "0") == "1"
+# text encoders captured as a graph per batch shape (CLIPTextEncoder.encode(graphs=True));
+# opt-in (CASSMANTLE_TEXT_GRAPH=1): no measured gain (profiles/r3_fusions_ab.txt)
+_TEXT_GRAPH = os.environ.get("CASSMANTLE_TEXT_GRAPH", "0") == "1"
 # Batch branches of the UNet evaluation: the CFG batch (uncond rows | cond rows) runs as this many
 # independent row ranges, each on its own stream, forked and joined inside the captured step
 # graph.  A batch-8 SD-1.5 step leaves most of the chip idle in its latency-bound kernels (the
@@ -191,11 +194,11 @@ class StableDiffusion:
         """-> ctx [2B, 77, D] ordered (uncond..., cond...), optional SDXL add-embeds."""
         texts = [negative] * len(prompts) + list(prompts)
         if len(self.text_encoders) == 1:
-            ctx, _ = self.text_encoders[0].encode(texts, self.device)
+            ctx, _ = self.text_encoders[0].encode(texts, self.device, graphs=self.use_graphs and _TEXT_GRAPH)
             return ctx, None
         hs, pooled = [], None
         for enc in self.text_encoders:
-            h, p = enc.encode(texts, self.device, output_hidden=-2)
+            h, p = enc.encode(texts, self.device, output_hidden=-2, graphs=self.use_graphs and _TEXT_GRAPH)
             hs.append(h)
             if p is not None:
                 pooled = p

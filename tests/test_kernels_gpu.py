@@ -941,3 +941,52 @@ def test_conv_halo_bitwise_repeatable(force_cfg):
     a = ops.conv2d(x, w, None)
     for _ in range(20):
         assert torch.equal(ops.conv2d(x, w, None), a)
+
+
+@pytest.mark.parametrize("M,N,K,resid", [(2048, 1280, 1280, True), (512, 1280, 1280, False), (300, 640, 320, True)])
+def test_gemm_row_stats_feed_folded_layernorm(M, N, K, resid):
+    """a producer GEMM's epilogue accumulates the LayerNorm row statistics of its stored output
+    (``row_stats``), and the LayerNorm-folded consumer reads them (``ln_linear(row_stats=)``)
+    instead of running a statistics pass: same result as LayerNorm + GEMM"""
+    from cassmantle_amd.ops._ext import ext
+    x = rnd(M, K, seed=141)
+    w = rnd(N, K, scale=K ** -0.5, seed=142)
+    b = rnd(N, scale=0.1, seed=143)
+    r = rnd(M, N, seed=144) if resid else None
+    rs = ops.new_stats(1, M, DEV).view(M, 2)
+    y = ops.linear(x, w, b, residual=r, row_stats=rs)
+    assert tuple(ext().gemm_last_plan())[1] == 1          # row statistics: never split-K
+    exp = ref.linear(x, w, b, residual=r)
+    assert rel_err(y, exp) < 1e-2
+    yf = y.float()
+    got = ops.stats_to_float(rs.view(1, M, 2))[0].float()
+    assert torch.allclose(got[:, 0], yf.sum(1), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(got[:, 1], (yf * yf).sum(1), rtol=1e-4, atol=1e-1)
+    # consumer: LayerNorm(y) @ W2^T through the fold, statistics from the producer
+    g = rnd(N, seed=145) * 0.5 + 1
+    be = rnd(N, seed=146) * 0.1
+    w2 = rnd(3 * N // 2 // 8 * 8, N, scale=N ** -0.5, seed=147)
+    fold = ops.ln_fold(g, be, w2)
+    out = ops.ln_linear(y, g, be, 1e-5, w2, fold=fold, row_stats=rs)
+    exp2 = ref.linear(ref.layer_norm(y, g, be, 1e-5), w2)
+    assert rel_err(out, exp2) < 1e-2
+    out_pass = ops.ln_linear(y, g, be, 1e-5, w2, fold=fold)      # the statistics-pass path
+    assert rel_err(out, out_pass) < 5e-3      # (bf16 rounding of two different kernels)
+
+
+@pytest.mark.parametrize("B,S,C,N", [(2, 4096, 320, 320), (2, 1024, 640, 640), (1, 256, 320, 192)])
+def test_gn_linear_folds_groupnorm_into_areg(B, S, C, N):
+    """GroupNorm (producer statistics, no SiLU) applied to the A rows inside the A-in-registers
+    GEMM (transformer GroupNorm -> proj_in) vs GroupNorm then GEMM in fp32"""
+    from cassmantle_amd.ops._ext import ext
+    x = rnd(B, S, C, seed=151) * 1.5 + 0.3
+    st = ops.new_stats(B, C, DEV)
+    ops.channel_stats_ref(x, st)
+    g = rnd(C, seed=152) * 0.5 + 1
+    be = rnd(C, seed=153) * 0.2
+    w = rnd(N, C, scale=C ** -0.5, seed=154)
+    b = rnd(N, scale=0.1, seed=155)
+    out = ops.gn_linear(x, st, g, be, 32, 1e-6, w, b)
+    assert tuple(ext().gemm_last_plan())[0] == 15
+    exp = ref.linear(ref.group_norm(x.float(), 32, g.float(), be.float(), 1e-6, False).to(torch.bfloat16), w, b)
+    assert rel_err(out, exp) < 1e-2

@@ -302,3 +302,16 @@ def test_sd15_branches_end_to_end_matches_one_batch():
     mse = ((a - b) ** 2).mean().item()
     psnr = 10 * math.log10(255.0 ** 2 / max(mse, 1e-12))
     assert psnr > 38.0, psnr
+
+
+def test_clip_encode_graph_matches_eager():
+    """the graph-captured text encoder (one capture per batch shape, replayed per generation)
+    gives the eager encoder's output, and a second replay with other prompts is not stale"""
+    from cassmantle_amd.models.text import CLIP_L, CLIPTextEncoder
+    enc = CLIPTextEncoder(CLIP_L, seed=2).cuda()
+    with torch.no_grad():
+        for texts in (["a lantern by the river", "blurry"], ["an ember in the tower", "fake, abstract"]):
+            h_e, _ = enc.encode(texts, "cuda", output_hidden=-2)
+            h_g, _ = enc.encode(texts, "cuda", output_hidden=-2, graphs=True)
+            torch.cuda.synchronize()
+            assert torch.equal(h_e, h_g)
