@@ -71,14 +71,20 @@ CM_DEVICE void add4(float* o, uint2 v) {
 // mean_m * wsum[n..n+3]) for the W rows n..n+3
 CM_DEVICE float2 ln_row(const GemmArgs& p, int m) {
   if (p.ln_rows_fx != nullptr) {
+    // fp32 decode (the fp64 form pushed the 256x256 ping-pong tiles into scratch): the fixed-
+    // point sums are exact; mean = s / K, var = q / K - mean^2 in fp32 (LayerNorm inputs here
+    // are residual streams with |mean| ~ std, far from the cancellation range)
     const longlong2 v = reinterpret_cast<const longlong2*>(p.ln_rows_fx)[m];
-    const double inv = 1.0 / p.K;
-    const double mean = (double)v.x * (inv / STAT_SCALE_SUM);
-    double var = (double)v.y * (inv / STAT_SCALE_SQ) - mean * mean;
-    var = var > 0.0 ? var : 0.0;
-    return make_float2((float)mean, rsqrtf((float)var + p.ln_eps));
+    const float inv = 1.f / (float)p.K;
+    const float mean = (float)v.x * (inv * (float)(1.0 / STAT_SCALE_SUM));
+    const float var = fmaxf((float)v.y * (inv * (float)(1.0 / STAT_SCALE_SQ)) - mean * mean, 0.f);
+    return make_float2(mean, rsqrtf(var + p.ln_eps));
   }
   return reinterpret_cast<const float2*>(p.ln_rows)[m];
+}
+CM_DEVICE void ln_apply4(float2 ms, const float* __restrict__ wsum, float* o) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, wsum[r], o[r]);
 }
 CM_DEVICE void ln_fold4(const GemmArgs& p, int m, int wn, float* o) {
   const float2 ms = ln_row(p, m);
@@ -196,6 +202,9 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         const int ml = wm * (BM / WM) + 16 * j + fr;
         const int m = m0 + ml;
         const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
+        // folded LayerNorm: this row's (mean, rstd), once per row (not per 4-column group)
+        const bool lnf = (p.ln_rows != nullptr || p.ln_rows_fx != nullptr) && m < p.M;
+        const float2 lnm = lnf ? ln_row(p, m) : make_float2(0.f, 1.f);
         if constexpr (GEGLU) {
 #pragma unroll
           for (int pi = 0; pi < TI / 2; ++pi) {
@@ -204,7 +213,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
             float o[4], hh[4], gg[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) { hh[r] = acc[2 * pi][j][r]; gg[r] = acc[2 * pi + 1][j][r]; }
-            if ((p.ln_rows || p.ln_rows_fx) && n < p.N && m < p.M) { ln_fold4(p, m, n, hh); ln_fold4(p, m, p.N + n, gg); }
+            if (lnf && n < p.N) { ln_apply4(lnm, p.ln_wsum + n, hh); ln_apply4(lnm, p.ln_wsum + p.N + n, gg); }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float h = hh[r], g = gg[r];
@@ -219,7 +228,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
             const int nl = wn * (BN / WN) + 16 * i + 4 * fq;
             const int n = n0 + nl;
             float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if ((p.ln_rows || p.ln_rows_fx) && n < p.N && m < p.M) ln_fold4(p, m, n, o);
+            if (lnf && n < p.N) ln_apply4(lnm, p.ln_wsum + n, o);
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] *= p.alpha;
             if (n < p.N && m < p.M) {
