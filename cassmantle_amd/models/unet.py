@@ -119,8 +119,10 @@ _GN_FOLD = os.environ.get("CASSMANTLE_GN_FOLD", "1") == "1"
 
 
 def _row_stats_wanted(x: torch.Tensor) -> bool:
+    # (>= 1024 rows: the producers of smaller inputs -- the SD-1.5 8^2 mid block -- run split-K,
+    # which a row-statistics epilogue forbids; there the statistics pass is cheaper)
     return (_LN_ROWSTATS and x.device.type == "cuda" and ops.get_mode() == "hip" and ops.LN_FOLD_MODE == 1
-            and x.shape[-1] not in (320, 640) and x.shape[-1] % 8 == 0 and x.numel() // x.shape[-1] > 8)
+            and x.shape[-1] not in (320, 640) and x.shape[-1] % 8 == 0 and x.numel() // x.shape[-1] >= 1024)
 
 
 # fp8 self-attention K/V emitted by the QKV projection's epilogue (no per-call pack kernel);
@@ -203,7 +205,9 @@ class Transformer2D(nn.Module):
     def forward(self, x, ctx, fp8=False, arena: Optional[StatsArena] = None, xs=None):
         B, H, W, C = x.shape
         hrs = None
-        if (_GN_FOLD and xs is not None and C in (320, 640) and (H * W) % 256 == 0 and x.device.type == "cuda"
+        # (C = 320 only: at C = 640 the A-in-registers kernel runs the N = 640 proj_in at 41 us
+        # vs 14.5 + 9.8 us for the ping-pong GEMM + GroupNorm apply; profiles/r3_prof_sd15_per_eval_final.txt)
+        if (_GN_FOLD and xs is not None and C == 320 and (H * W) % 256 == 0 and x.device.type == "cuda"
                 and ops.get_mode() == "hip"):
             # GroupNorm folded into proj_in (A-in-registers GEMM): no GroupNorm pass over x
             n = self.norm
