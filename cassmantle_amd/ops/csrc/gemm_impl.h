@@ -1033,6 +1033,8 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 17: return launch_t<128, 64, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
       case 18: return launch_t<128, 128, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
       case 19: return launch_t<128, 160, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
+      case 26: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true>(p, ws, s);
+      case 27: return launch_t<128, 64, 4, 2, CONV, false, false, 3, true>(p, ws, s);
       default: break;
     }
   }

@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cassmantle_amd import ops  # noqa: E402
 from cassmantle_amd.ops._ext import ext  # noqa: E402
 
-CFGS = list(range(26))   # 15 = A-in-registers short-K kernel, 16 = 128x80 deep ring, 17-19 register-staged, 20 = pp 128x160, 21 = pp 128x128, 22/23 = pp 128x64 / 256x64, 24/25 = halo-staged 3x3 conv 256x160 / 128x160
+CFGS = list(range(28))   # 15 = A-in-registers short-K kernel, 16 = 128x80 deep ring, 17-19 register-staged, 20 = pp 128x160, 21 = pp 128x128, 22/23 = pp 128x64 / 256x64, 24/25 = halo-staged 3x3 conv 256x160 / 128x160, 26/27 = 8-wave 128x80 / 128x64 deep ring
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
 
 
@@ -72,7 +72,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(ops.__file__), "gemm_tuning.json"))
     ap.add_argument("--merge", action="store_true", help="keep existing entries of other shapes")
+    ap.add_argument("--cfgs", default=None,
+                    help="comma list of tile configs to time (default: all); with --merge the shape's "
+                         "existing table plan is always an arm, so a partial sweep only adds new winners")
     a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",")] if a.cfgs else CFGS
     os.environ["CASSMANTLE_GEMM_TUNE"] = "0"
     ops.set_mode("hip")
     ext().gemm_tune_clear()
@@ -96,7 +100,11 @@ def main():
             ext().gemm_set_override(-1, 0)
             fn()
             arms[tuple(ext().gemm_last_plan())] = "auto"
-            for c in CFGS:
+            if key in entries:                      # the existing table plan (merge)
+                ext().gemm_set_override(entries[key]["cfg"], entries[key]["split"])
+                fn()
+                arms.setdefault(tuple(ext().gemm_last_plan()), "table")
+            for c in cfgs:
                 for sp in SPLITS:
                     ext().gemm_set_override(c, sp)
                     fn()
@@ -117,7 +125,7 @@ def main():
                     "auto_us": round(med[auto_plan], 2), "best": list(best), "best_us": round(med[best], 2),
                     "gain": round(gain, 3), "arms": len(arms)}
             print(json.dumps(line), flush=True)
-            if best != auto_plan and gain > 1.02:
+            if best != auto_plan and gain > 1.02 and (key not in entries or arms[best] != "table"):
                 entries[key] = {"key": key, "cfg": best[0], "split": best[1], "us": round(med[best], 2),
                                 "auto_us": round(med[auto_plan], 2), "model": model}
         ext().gemm_record_keys(False)

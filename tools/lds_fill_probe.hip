@@ -25,7 +25,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <int WAVES, int DEPTH>
+template <int WAVES, int DEPTH, bool ROWS>
 __global__ void __launch_bounds__(64 * WAVES, 1) fill(const uint4* __restrict__ src, long long window_bytes, int iters,
                                                       long long* __restrict__ cyc) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
@@ -41,7 +41,11 @@ __global__ void __launch_bounds__(64 * WAVES, 1) fill(const uint4* __restrict__ 
   int p = wave;
 #pragma unroll 1
   for (int i = 0; i < iters; ++i) {
-    const int off = base + ((p % pieces) * 1024) + lane * 16;
+    // ROWS: a GEMM tile's access pattern: one piece = 8 rows x 128 B (64 bf16 of K) of a
+    // row-major [rows, 1280] bf16 matrix (2560 B row stride), k-chunks of a row block in order
+    const int q = ROWS ? p % (pieces / 20 * 20) : p % pieces;
+    const int off = ROWS ? base + ((q / 20) * 8 + (lane >> 3)) * 2560 + (q % 20) * 128 + (lane & 7) * 16
+                         : base + q * 1024 + lane * 16;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(ring + (i % DEPTH) * 64), 16, off, 0, 0, 0);
     wait_vm<DEPTH - 1>();
     p += WAVES;
@@ -52,10 +56,10 @@ __global__ void __launch_bounds__(64 * WAVES, 1) fill(const uint4* __restrict__ 
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int WAVES, int DEPTH>
+template <int WAVES, int DEPTH, bool ROWS = false>
 void run(const uint4* src, long long window, long long* d_cyc, int nblk) {
   const int iters = 4096;
-  auto* k = &fill<WAVES, DEPTH>;
+  auto* k = &fill<WAVES, DEPTH, ROWS>;
   const size_t lds = (size_t)WAVES * DEPTH * 1024;
   CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k, dim3(nblk), dim3(64 * WAVES), lds, 0, src, window, iters, d_cyc);
@@ -74,9 +78,9 @@ void run(const uint4* src, long long window, long long* d_cyc, int nblk) {
   std::sort(cyc.begin(), cyc.end());
   const double bytes_per_wg = (double)WAVES * iters * 1024;
   const double med = (double)cyc[nblk / 2];
-  printf("{\"waves\": %d, \"depth\": %d, \"in_flight_kib_per_cu\": %d, \"window_mib\": %.0f, \"B_per_cycle_per_cu\": %.1f, "
+  printf("{\"access\": \"%s\", \"waves\": %d, \"depth\": %d, \"in_flight_kib_per_cu\": %d, \"window_mib\": %.0f, \"B_per_cycle_per_cu\": %.1f, "
          "\"chip_TBps\": %.2f}\n",
-         WAVES, DEPTH, WAVES * (DEPTH - 1), window / 1048576.0, bytes_per_wg / med,
+         ROWS ? "8x128B-rows" : "1KiB-contiguous", WAVES, DEPTH, WAVES * (DEPTH - 1), window / 1048576.0, bytes_per_wg / med,
          bytes_per_wg * nblk * reps / (ms * 1e-3) / 1e12);
 }
 
@@ -88,20 +92,26 @@ int main() {
   CK(hipMalloc(&src, window));
   CK(hipMemset(src, 1, window));
   CK(hipMalloc(&d_cyc, nblk * sizeof(long long)));
-  run<1, 2>(src, window, d_cyc, nblk);
-  run<1, 4>(src, window, d_cyc, nblk);
   run<1, 8>(src, window, d_cyc, nblk);
-  run<4, 2>(src, window, d_cyc, nblk);
   run<4, 4>(src, window, d_cyc, nblk);
-  run<4, 8>(src, window, d_cyc, nblk);
-  run<8, 4>(src, window, d_cyc, nblk);
-  run<8, 8>(src, window, d_cyc, nblk);
-  run<16, 4>(src, window, d_cyc, nblk);
   run<16, 8>(src, window, d_cyc, nblk);
   const long long small = 8LL << 20;     // 8 MiB: L2-resident (4 MiB per XCD, 32 CUs each)
+  run<1, 2>(src, small, d_cyc, nblk);
+  run<1, 4>(src, small, d_cyc, nblk);
+  run<1, 8>(src, small, d_cyc, nblk);
+  run<1, 16>(src, small, d_cyc, nblk);
+  run<2, 8>(src, small, d_cyc, nblk);
+  run<4, 2>(src, small, d_cyc, nblk);
   run<4, 4>(src, small, d_cyc, nblk);
+  run<4, 8>(src, small, d_cyc, nblk);
+  run<4, 16>(src, small, d_cyc, nblk);
+  run<8, 4>(src, small, d_cyc, nblk);
   run<8, 8>(src, small, d_cyc, nblk);
   run<16, 8>(src, small, d_cyc, nblk);
+  run<4, 4, true>(src, small, d_cyc, nblk);
+  run<4, 8, true>(src, small, d_cyc, nblk);
+  run<8, 8, true>(src, small, d_cyc, nblk);
+  run<16, 8, true>(src, small, d_cyc, nblk);
   CK(hipFree(src));
   CK(hipFree(d_cyc));
   return 0;
