@@ -458,7 +458,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   constexpr int THREADS = 64 * NW;
   constexpr int RR = 8 * NW;               // rows covered by one DMA round (8 per wave)
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NW == 4 || NW == 8 || NW == 16, "4, 8 or 16 waves");
   constexpr int TI = BN / WN / 16;         // n-subtiles per wave
   constexpr int TJ = BM / WM / 16;         // m-subtiles per wave
   static_assert(!GEGLU || (TI % 2 == 0), "geglu pairs");
@@ -1035,6 +1035,7 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 19: return launch_t<128, 160, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
       case 26: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true>(p, ws, s);
       case 27: return launch_t<128, 64, 4, 2, CONV, false, false, 3, true>(p, ws, s);
+      case 28: return launch_t<128, 64, 8, 2, CONV, false, false, 3, true>(p, ws, s);
       default: break;
     }
   }

@@ -8,5 +8,5 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
   -m gpu -k "_pp" > gpurun_out/t8w.log 2>&1 || { tail -30 gpurun_out/t8w.log; exit 1; }
 tail -2 gpurun_out/t8w.log
-timeout -k 10 300 python -u tools/probe_small_gemm.py --cfgs 3,16,26,27,22 --ks 320,640,1280,2560 | tee gpurun_out/probe8w.jsonl
-timeout -k 10 300 python -u tools/probe_small_gemm.py --m 8192 --n 640 --cfgs 3,16,26,27,22,21 --ks 640,1280 | tee -a gpurun_out/probe8w.jsonl
+timeout -k 10 300 python -u tools/probe_small_gemm.py --cfgs 3,16,26,27,28 --ks 320,640,1280,2560 | tee gpurun_out/probe8w.jsonl
+timeout -k 10 300 python -u tools/probe_small_gemm.py --m 8192 --n 640 --cfgs 3,26,27,28,21 --ks 640,1280 | tee -a gpurun_out/probe8w.jsonl
