@@ -44,13 +44,14 @@ constexpr int BK = 64;
 //   24 / 25: halo-staged 3x3 conv 256x160 / 128x160 (gemm_halo.h: one halo tile per 64-channel
 //       chunk serves all 9 taps; half the LDS-DMA bytes per k-tile of the CONV 2 path)
 //   28: 16-wave 128x64 (8x2 waves, wave 16x32, 3 stages): 16 waves issuing the DMA (48 B/cycle)
+//   29 / 30: 8-wave 128x128 (4x2 waves, wave 32x64) / 256x80 (8x1 waves, wave 32x80), 3 stages
 //   26 / 27: 8-wave 128x80 (8x1 waves, wave 16x80, 4-stage ring) / 128x64 (4x2 waves, 3 stages):
 //       the small-grid tiles with twice the waves issuing LDS-DMA.  A CU's LDS-DMA fill rate is
 //       set by the number of waves issuing it, not by the bytes in flight (4 waves: 22 B/cycle
 //       on the GEMM row pattern at any ring depth, 8 waves: 37; profiles/r3_lds_fill_probe.jsonl)
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 29;
+constexpr int kNumTiles = 31;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
 constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22 || c == 23; }
@@ -70,7 +71,8 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 128, 1.f, 512},   {128, 160, 1.f, 512},   {128, 160, 1.f, 256},
                                        {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512},
                                        {256, 160, 1.f, 256},   {128, 160, 1.f, 256},   {128, 80, 1.f, 256},
-                                       {128, 64, 1.f, 256},    {128, 64, 1.f, 256}};
+                                       {128, 64, 1.f, 256},    {128, 64, 1.f, 256},    {128, 128, 1.f, 256},
+                                       {256, 80, 1.f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a
 // 31-bit buffer offset (num_records), plain GEMMs and Cin % 64 convolutions without upsample

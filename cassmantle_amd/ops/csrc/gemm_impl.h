@@ -1036,6 +1036,8 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 26: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true>(p, ws, s);
       case 27: return launch_t<128, 64, 4, 2, CONV, false, false, 3, true>(p, ws, s);
       case 28: return launch_t<128, 64, 8, 2, CONV, false, false, 3, true>(p, ws, s);
+      case 29: return launch_t<128, 128, 4, 2, CONV, false, false, 3, true>(p, ws, s);
+      case 30: return launch_t<256, 80, 8, 1, CONV, false, false, 3, true>(p, ws, s);
       default: break;
     }
   }

@@ -505,7 +505,7 @@ def test_latent_step_matches_reference(sched):
 
 
 # ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
-PP_CFGS = [7, 8, 9, 10, 11, 12, 13, 14, 16, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28]   # ping-pong (7-10, 20-23), deep-ring (11-14, 16, 8-wave 26/27, 16-wave 28), register-staged (17-19)
+PP_CFGS = [7, 8, 9, 10, 11, 12, 13, 14, 16, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28, 29, 30]   # ping-pong (7-10, 20-23), deep-ring (11-14, 16, 8-wave 26/27/29/30, 16-wave 28), register-staged (17-19)
 
 
 @pytest.fixture
