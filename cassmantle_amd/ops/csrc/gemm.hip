@@ -275,7 +275,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
       (force_cfg < kFirstPP || (is_pp_cfg(force_cfg) ? pp_elig : deep_elig))) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
-      else if (force_cfg >= kFirstDeep) best.cfg = 12;            // the deep-ring gated tile
+      else if (force_cfg >= kFirstDeep) best.cfg = force_cfg == 29 ? 29 : 12;   // the deep-ring gated tiles (4 / 8 waves)
       else if (force_cfg >= kFirstPP) best.cfg = force_cfg == 8 ? 8 : 9;   // the ping-pong gated tiles
       return best;
     }

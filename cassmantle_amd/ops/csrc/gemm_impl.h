@@ -1057,6 +1057,7 @@ void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
   if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) {
     if constexpr (BUF) {
       if (p.cfg == 12) return launch_t<128, 128, 2, 2, CONV, true, false, 4, true>(p, ws, s);
+      if (p.cfg == 29) return launch_t<128, 128, 4, 2, CONV, true, false, 3, true>(p, ws, s);   // 8-wave gated
     }
     if (p.cfg == 6) launch_st<256, 128, 4, 2, CONV, true, false, BUF>(p, ws, s);
     else launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);
