@@ -119,8 +119,72 @@ def scorer_bench(device) -> dict:
             "cpu_numpy_cosine_1pair_p50_ms": round(float(np.percentile(lat_np, 50)), 5)}
 
 
+def _visible_gpus() -> int:
+    """Device count WITHOUT initialising the GPU (on this ROCm image ``device_count`` does not
+    create a HIP context, so the launcher may still start fresh rank processes afterwards)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args) -> int:
+    """``bench.py --gpus N`` with no torchrun environment: start N fresh rank processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; RCCL on GPUs, gloo on the CPU) before
+    this process makes any GPU call, relay rank 0's JSON line and fail if any rank fails.
+    Every rank's stdout/stderr is inherited; only rank 0 prints the result line."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # host threads per rank (torchrun's default is 1): N ranks must not each spin up a
+        # thread per core of the machine
+        env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:           # peers would block in a collective forever
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main() -> int:
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"[bench] WORLD_SIZE={env_world} disagrees with --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if env_world is None and args.gpus > 1:
+        n_vis = _visible_gpus()
+        if n_vis and args.gpus > n_vis:
+            print(f"[bench] --gpus {args.gpus} exceeds the {n_vis} visible GPU(s)", file=sys.stderr)
+            return 2
+        return launch_ranks(args)
+    if env_world is None and args.gpus < 1:
+        print("[bench] --gpus must be >= 1", file=sys.stderr)
+        return 2
     if args.baseline:
         os.environ["CASSMANTLE_OPS"] = "torch"
     import numpy as np

@@ -80,6 +80,10 @@ class GameConfig:
     rank_stale_s: float = 30.0            # a heartbeat older than this marks the rank dead
     round_timeout_s: float = 600.0        # a generation round running longer degrades to local
     exit_on_rank_failure: bool = False    # after degrading: snapshot + exit 3 for a supervisor
+    # supervised groups: once EVERY device is retired, rounds repeat (the reference's fallback,
+    # src/backend.py:211-215) and the retired devices are re-probed after this long (doubling
+    # per failed probe, capped at 1 h) instead of being lost for the life of the process
+    device_reprobe_s: float = 120.0
     # --- multi-GPU guess scoring (parallel/scoring.py) ---
     score_topology: str = "central"       # central (rank 0 scores) | sharded (C1 broadcast + C3 gather)
     score_shard_min: int = 256            # sharded: smaller micro-batches are still scored on rank 0

@@ -123,18 +123,27 @@ class RankWorker:
             self._comm = torch.cuda.Stream(device=dev)
         return self._comm
 
-    def _generate_into(self, mine_jobs: List[GenJob], buf: torch.Tensor, ok: torch.Tensor, comm) -> None:
+    def _generate_into(self, mine_jobs: List[GenJob], buf: torch.Tensor, ok: torch.Tensor, comm):
+        """Generate this rank's images into ``buf`` / ``ok``.  Returns the event that marks the
+        device work done (None when the work is already complete on return)."""
         prompts, seeds = [j.prompt for j in mine_jobs], [j.seed for j in mine_jobs]
         n = len(mine_jobs)
         gen_dev = getattr(self.gen, "generate_device", None)
-        if gen_dev is not None and comm is not None:
-            out = gen_dev(prompts, self.negative, seeds)          # images stay in HBM
-            comm.wait_event(out.event)                             # ordered after the VAE decode
-            with torch.cuda.stream(comm):
-                out.images.record_stream(comm)
-                buf[:n].copy_(out.images)
-                ok[:n].copy_(out.finite.to(torch.uint8).expand(n) if out.finite is not None else torch.ones_like(ok[:n]))
-            return
+        if gen_dev is not None:
+            out = gen_dev(prompts, self.negative, seeds)          # queued; images stay on the device
+            if comm is not None:
+                comm.wait_event(out.event)                         # ordered after the VAE decode
+                with torch.cuda.stream(comm):
+                    out.images.record_stream(comm)
+                    buf[:n].copy_(out.images)
+                    ok[:n].copy_(out.finite.to(torch.uint8).expand(n) if out.finite is not None
+                                 else torch.ones_like(ok[:n]))
+                return out.event
+            # host-side buffers (gloo): the images must be complete before they are read
+            wait_event(out.event)
+            buf[:n].copy_(out.images)
+            ok[:n] = int(bool(out.finite.reshape(-1)[0])) if out.finite is not None else 1
+            return None
         imgs = self.gen.generate(prompts, self.negative, seeds)
         host = torch.from_numpy(np.ascontiguousarray(np.stack(imgs)))
         if comm is not None:
@@ -144,6 +153,7 @@ class RankWorker:
         else:
             buf[:n].copy_(host)
             ok[:n] = 1
+        return None
 
     def run_round(self, jobs: Optional[List[GenJob]], round_id: int = 0) -> Optional[Dict[Tuple[str, int], np.ndarray]]:
         """Collective: every rank must call it.  Rank 0 passes the job list (or STOP); others
@@ -169,7 +179,11 @@ class RankWorker:
             comm.wait_stream(torch.cuda.current_stream(dev))      # the zero-fills above
         if mine:
             try:
-                self._generate_into([jobs[i] for i in mine], buf, ok, comm)
+                done = self._generate_into([jobs[i] for i in mine], buf, ok, comm)
+                # progress is published only once the DEVICE work finished: a wedged
+                # GPU then never reports this round, so the supervisor can blame its worker
+                if done is not None:
+                    wait_event(done)
             except Exception as e:  # noqa: BLE001 - a failed rank must still join the collectives
                 log.error("[ERROR] rank %d generation failed: %s", rank, e)
                 if comm is not None:
@@ -229,6 +243,14 @@ class RankWorker:
         while True:
             if self.run_round(None) == STOP:
                 return
+
+
+def wait_event(ev, poll_s: float = 0.0005) -> None:
+    """Block until ``ev`` (a ``torch.cuda.Event`` or anything with ``query()``) completed.  Polls
+    instead of ``Event.synchronize()``: the thread stays a plain Python loop (heart-beat threads and
+    signal handlers keep running while a wedged device never completes the event)."""
+    while not ev.query():
+        time.sleep(poll_s)
 
 
 class _nullctx:

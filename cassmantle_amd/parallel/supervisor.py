@@ -22,7 +22,10 @@ lock generates; a crashed holder's lock expires (120 s TTL) and any surviving wo
   torn down (SIGKILL: a collective with a dead peer cannot be cancelled in-process) and
   respawned on the remaining healthy devices, with the rooms re-sharded over the survivors;
 * a device is retired when its worker died or hung; a failure no worker can be blamed for
-  restarts the group on the same devices (``max_restarts_without_culprit`` times).
+  restarts the group on the same devices (``max_restarts_without_culprit`` times);
+* with every device retired the rooms' rounds repeat (the reference's fallback), or a ``local``
+  generator serves them, and the retired devices are re-probed with a fresh group after
+  ``reprobe_s`` (doubling per failed probe): a transient fault does not cost the GPUs forever.
 
 The legacy ``torchrun`` layout (front-end inside rank 0, ``serve.py`` under torchrun) is still
 supported; there a dead rank can only degrade the node to rank 0's GPU.
@@ -224,7 +227,8 @@ class GroupSupervisor:
                  window_s: float = 0.3, round_timeout_s: float = 600.0, stale_s: float = 30.0,
                  heartbeat_s: float = 0.5, start_timeout_s: float = 900.0, watch_period_s: float = 0.2,
                  max_restarts_without_culprit: int = 2, local: Optional[ImageGenerator] = None,
-                 worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None) -> None:
+                 worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None,
+                 reprobe_s: float = 120.0) -> None:
         self.cfg = cfg
         self.all_devices = list(devices)
         self.healthy = list(devices)
@@ -250,6 +254,10 @@ class GroupSupervisor:
         self.gather_us: List[float] = []
         self._blind = 0
         self._round_id = 0
+        self.reprobe_s = reprobe_s
+        self._probe_backoff = reprobe_s
+        self._next_probe = float("inf")
+        self.probes: List[Dict[str, Any]] = []
         self._q: "queue.Queue" = queue.Queue()
         self._closed = False
         self._ready = threading.Event()
@@ -297,6 +305,8 @@ class GroupSupervisor:
                 for d in list(self.healthy):
                     self.retired[d] = "repeated group failures"
                 self.healthy.clear()
+        if not self.healthy and self._next_probe == float("inf"):
+            self._next_probe = time.time() + self._probe_backoff
         log.error("[ERROR] worker group epoch %d failed (%s); retired %s; healthy %s", self.epoch, reason, devs,
                   self.healthy)
 
@@ -314,6 +324,31 @@ class GroupSupervisor:
                 if self.group is not None:
                     self.group.kill()
                 self.group = None
+
+    def _maybe_reprobe(self) -> None:
+        """With no live group: once the back-off has passed, put every retired device back and
+        try a fresh group on them (a failed probe retires them again and doubles the back-off)."""
+        if self.group is not None or not self.retired or self._closed or time.time() < self._next_probe:
+            return
+        back = [d for d in self.all_devices if d in self.retired]
+        log.info("[INFO] re-probing retired devices %s", back)
+        t0 = time.time()
+        for d in back:
+            self.retired.pop(d, None)
+        self.healthy = [d for d in self.all_devices if d not in self.retired]
+        self._blind = 0
+        self._next_probe = float("inf")
+        try:
+            self._start_group()
+        except GroupFailure as e:
+            self._restart(e.culprits, str(e))
+        ok = self.group is not None
+        self.probes.append({"devices": back, "ok": ok, "s": round(time.time() - t0, 3)})
+        if ok:
+            self._probe_backoff = self.reprobe_s
+        else:
+            self._probe_backoff = min(2 * self._probe_backoff, 3600.0)
+            self._next_probe = time.time() + self._probe_backoff
 
     # ------------------------------------------------------------------ requests
     def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
@@ -403,6 +438,8 @@ class GroupSupervisor:
                     break
                 batch.append(nxt)
             if self.group is None:
+                self._maybe_reprobe()
+            if self.group is None:
                 self._serve_without_group(batch)
                 continue
             jobs, spans = [], []
@@ -427,14 +464,22 @@ class GroupSupervisor:
                     if not fut.done():
                         fut.set_exception(ImageGenerationError(f"generation round failed: {e}"))
                 self._restart(culprits, str(e))
+            except Exception as e:  # noqa: BLE001 - unexpected (message shape, pickling): never kill this thread
+                log.exception("[ERROR] supervisor round failed unexpectedly")
+                for *_, fut in spans:
+                    if not fut.done():
+                        fut.set_exception(ImageGenerationError(f"generation round failed: {type(e).__name__}: {e}"))
+                self._restart([], f"unexpected {type(e).__name__}: {e}")
         if self.group is not None:
             self.group.stop()
             self.group = None
 
     def _serve_without_group(self, batch) -> None:
+        """No live group: a ``local`` generator serves the batch, otherwise each room's round
+        repeats (its request fails fast; the room keeps its content, src/backend.py:211-215)."""
         for room, prompts, seeds, fut in batch:
             if self.local is None:
-                fut.set_exception(ImageGenerationError("no healthy generation device left"))
+                fut.set_exception(ImageGenerationError("no healthy generation device left: the round repeats"))
                 continue
             try:
                 fut.set_result(self.local.generate(prompts, self.negative, seeds))
@@ -453,7 +498,7 @@ class GroupSupervisor:
 
     def status(self) -> Dict[str, Any]:
         return {"epoch": self.epoch, "live_devices": self.live_devices(), "retired": dict(self.retired),
-                "rounds": self.rounds, "failures": list(self.failures),
+                "rounds": self.rounds, "failures": list(self.failures), "probes": list(self.probes),
                 "gather_us_p50": float(np.median(self.gather_us)) if self.gather_us else None}
 
 

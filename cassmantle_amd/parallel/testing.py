@@ -6,7 +6,9 @@ configured through the worker environment:
 * ``CASSMANTLE_FAULT_SLOT``: the device label (``cpu:1``, ``cuda:3``) whose worker misbehaves;
 * ``CASSMANTLE_FAULT``: ``kill`` (the process exits mid-round, like an OOM kill or a driver
   crash), ``hang`` (the generation never returns but the process keeps heart-beating, like a
-  wedged GPU kernel), ``fail`` (the generation raises);
+  wedged GPU kernel), ``fail`` (the generation raises), ``async_hang`` (``generate_device``
+  returns at once, as the real pipeline does when it only QUEUES the work, but its completion
+  event never fires: a GPU wedged inside the denoise graph);
 * ``CASSMANTLE_FAULT_TRIGGER``: a file; the fault fires only once it exists.
 
 Every image carries the generating slot's index in its top-left 8x8 block (value
@@ -46,8 +48,36 @@ class StampedGenerator(SolidImageGenerator):
         return out
 
 
+class _Done:
+    def query(self) -> bool:
+        return True
+
+
+class _Never:
+    """A device event of work that never completes."""
+
+    def query(self) -> bool:
+        return False
+
+
+class AsyncStampedGenerator(StampedGenerator):
+    """``StampedGenerator`` with the device-resident interface of the SD pipeline
+    (``generate_device`` -> ``DeviceImages``), host tensors standing in for HBM."""
+
+    def generate_device(self, prompts, negative_prompt, seeds):
+        import numpy as np
+        import torch
+        from ..pipeline import DeviceImages
+        if self._armed() and self.fault_mode == "async_hang":
+            img = torch.zeros((len(prompts), self.resolution, self.resolution, 3), dtype=torch.uint8)
+            return DeviceImages(img, None, _Never())
+        img = torch.from_numpy(np.stack(self.generate(prompts, negative_prompt, seeds)))
+        return DeviceImages(img, None, _Done())
+
+
 def stamped_generator(cfg, device: str, spec) -> StampedGenerator:
-    return StampedGenerator(spec.slot or device, res=cfg.model.resolution)
+    cls = AsyncStampedGenerator if os.environ.get("CASSMANTLE_FAULT") == "async_hang" else StampedGenerator
+    return cls(spec.slot or device, res=cfg.model.resolution)
 
 
 def slot_of(img) -> int:

@@ -369,9 +369,17 @@ class StableDiffusion:
             # flag is checked before the uint8 decode, where NaN/Inf would silently become a
             # garbage image)
             st = self._last_state
-            z = st.z if st.z.shape == x.shape else torch.empty(x.shape, device=x.device, dtype=self.dtype)
-            ops.finalize_latents(x, z, st.finite)
-            self.last_finite = st.finite
+            if self.decode_stream is None:
+                z, finite = st.z, st.finite
+            else:
+                # the decode of this generation runs on decode_stream, concurrently with the next
+                # generation's finalize_latents on self.stream: fresh buffers per generation, so
+                # the next one cannot overwrite the latents (or flag) a running decode reads
+                # (record_stream below only keeps the allocator from reusing them)
+                z = torch.empty(x.shape, device=x.device, dtype=self.dtype)
+                finite = torch.empty((16,), device=x.device, dtype=torch.uint8)[:1]
+            ops.finalize_latents(x, z, finite)
+            self.last_finite = finite
             self.last_latents = z
             if self.decode_stream is None:
                 with span("decode", self.stream):
@@ -381,6 +389,7 @@ class StableDiffusion:
             self.decode_stream.wait_stream(self.stream)
             with torch.cuda.stream(self.decode_stream), span("decode", self.decode_stream):
                 z.record_stream(self.decode_stream)
+                self.last_finite.record_stream(self.decode_stream)
                 img = self.vae.decode_uint8(z)
             out_stream = self.decode_stream
         self.out_stream = out_stream

@@ -131,8 +131,11 @@ def _serve_supervised(cfg, args) -> int:
     room_ids = [""] + [str(i) for i in range(1, max(cfg.game.num_rooms, n))]
     cfg.game.num_rooms = len(room_ids)
     devices = [f"cuda:{i}" for i in range(n)]
+    # no ``local`` generator: with every GPU retired the rounds repeat (the reference's fallback)
+    # until a re-probe brings devices back (cfg.game.device_reprobe_s)
     sup = GroupSupervisor(cfg, devices, room_ids, round_timeout_s=cfg.game.round_timeout_s,
-                          stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s)
+                          stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s,
+                          reprobe_s=cfg.game.device_reprobe_s)
     sup.wait_ready()
     svc = build_service(cfg, image_gen_for_room=lambda rid: SupervisedImageGenerator(sup, rid), room_ids=room_ids)
     app = create_app(svc, cfg)

@@ -1,0 +1,52 @@
+"""The headline harness contract (``bench.py``): ``--gpus N`` starts N rank processes by itself
+(no torchrun needed), the rank count must agree with a torchrun environment, and rank 0 prints
+one JSON line whose ``value`` is the whole-job aggregate.  CPU: gloo ranks on the tiny model."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    env["CUDA_VISIBLE_DEVICES"] = ""          # CPU ranks (gloo) even where a GPU is visible
+    env["HIP_VISIBLE_DEVICES"] = ""
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    r = _run(["--gpus", "2", "--model", "tiny", "--steps", "1", "--warmup", "0", "--no-score"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout                 # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2
+    assert out["comm"] == {"backend": "gloo", "world_size": 2}
+    assert [p["rank"] for p in out["per_rank"]] == [0, 1]
+    assert out["config"]["global_batch"] == 8
+    # whole-job aggregate: 2 ranks x 4 images x 1 step over the slowest rank's time
+    assert abs(out["value"] - 8 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.01
+
+
+def test_bench_world_size_mismatch_fails():
+    r = _run(["--gpus", "2", "--model", "tiny", "--steps", "1", "--warmup", "0", "--no-score"],
+             env_extra={"WORLD_SIZE": "1", "RANK": "0"}, timeout=120)
+    assert r.returncode == 2
+    assert "disagrees" in r.stderr
+
+
+def test_bench_failing_rank_fails_the_job():
+    # an unknown model raises in every rank: the launcher must exit non-zero, not hang
+    r = _run(["--gpus", "2", "--model", "nope", "--steps", "1", "--warmup", "0", "--no-score"], timeout=120)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)

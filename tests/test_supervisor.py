@@ -36,7 +36,7 @@ def _cfg(rooms):
     return cfg
 
 
-@pytest.mark.parametrize("fault", ["kill", "hang"])
+@pytest.mark.parametrize("fault", ["kill", "hang", "async_hang"])
 def test_dead_worker_retired_survivors_take_over(fault):
     from fastapi.testclient import TestClient
     from cassmantle_amd.api.app import create_app
@@ -118,3 +118,35 @@ def test_generation_failure_on_one_worker_keeps_group():
             sup.close()
     assert res == {"": 0, "1": "ImageGenerationError", "2": 0, "3": "ImageGenerationError"}, res
     assert st["epoch"] == 1 and not st["retired"] and st["gather_us_p50"] is None
+
+
+def test_every_device_lost_rounds_repeat_then_reprobe():
+    """the only worker dies: its rooms' rounds repeat (fail fast, no hang), and after the re-probe
+    back-off a fresh group on the retired device serves again"""
+    import time
+    from cassmantle_amd.game.content import ImageGenerationError
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1"]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault")
+        open(trig, "w").close()
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:0", "CASSMANTLE_FAULT": "kill", "CASSMANTLE_FAULT_TRIGGER": trig}
+        sup = GroupSupervisor(_cfg(rooms), ["cpu:0"], rooms, gen_factory="cassmantle_amd.parallel.testing:stamped_generator",
+                              window_s=0.1, worker_env=env, start_timeout_s=240, reprobe_s=2.0)
+        try:
+            assert sup.wait_ready(240)
+            with pytest.raises(ImageGenerationError):
+                sup.submit("", ["p"], [1]).result(timeout=120)
+            os.remove(trig)                                   # the fault is gone
+            t0 = time.time()
+            with pytest.raises(ImageGenerationError, match="repeats"):
+                sup.submit("1", ["p"], [2]).result(timeout=30)
+            assert time.time() - t0 < 5                       # fails fast: no group, no wait
+            time.sleep(2.5)
+            img = sup.submit("1", ["p"], [3]).result(timeout=240)
+            st = sup.status()
+        finally:
+            sup.close()
+    assert slot_of(img[0]) == 0
+    assert st["epoch"] == 2 and st["live_devices"] == ["cpu:0"] and not st["retired"], st
+    assert [p["ok"] for p in st["probes"]] == [True], st

@@ -1,8 +1,8 @@
 #!/bin/bash
 # In-situ rocprofv3 kernel trace of the benchmark step for one model, summarised per UNet eval.
-#   tools/gpu_profile.sh NAME MODEL DENOISE_STEPS PER_UNITS [extra bench.py args...]
-# e.g. tools/gpu_profile.sh sd15 sd15 10 24          (warm-up + timed step = 2 x 12 UNet evals)
-#      tools/gpu_profile.sh sdxl sdxl 4 10 --batch 1  (2 x (4 Euler evals + 1 spare))
+#   tools/gpu/profile.sh NAME MODEL DENOISE_STEPS PER_UNITS [extra bench.py args...]
+# e.g. tools/gpu/profile.sh sd15 sd15 10 24          (warm-up + timed step = 2 x 12 UNet evals)
+#      tools/gpu/profile.sh sdxl sdxl 4 10 --batch 1  (2 x (4 Euler evals + 1 spare))
 # writes gpurun_out/prof_NAME_summary.txt (+ the raw trace under gpurun_out/prof_NAME/)
 set -o pipefail
 name=$1; model=$2; steps=$3; per=$4; shift 4
