@@ -199,7 +199,10 @@ class RankWorker:
             if comm is not None:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ev0.record(comm)
-            if W > 1:
+            # the collectives run whenever a process group exists, world size 1 included (a
+            # one-GPU supervised group: RCCL then gathers device-locally, a few µs)
+            grouped = dist.is_available() and dist.is_initialized()
+            if grouped:
                 if rank == 0:
                     gl = [torch.empty_like(buf) for _ in range(W)]
                     gk = [torch.empty_like(ok) for _ in range(W)]
@@ -226,7 +229,7 @@ class RankWorker:
         if comm is not None:
             comm.synchronize()
             self.last_gather_us = ev0.elapsed_time(ev1) * 1e3
-        if W > 1:
+        if grouped:
             dist.barrier()                                                              # C4
         if rank == 0:
             out = {}

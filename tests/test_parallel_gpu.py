@@ -1,0 +1,63 @@
+"""The RCCL data plane on a real GPU: the device-resident image path of
+``parallel.rooms.RankWorker`` (``generate_device`` -> comm stream fenced by the decode event ->
+RCCL gather to the leader -> one pinned device-to-host copy) in an in-process world-size-1 nccl
+group, compared with the host path ``generate()``; and one supervised worker group
+(``parallel.supervisor``) on ``cuda:0``: nccl init with ``device_id``, spawned worker, pipe."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rank_worker_nccl_world1_device_path_matches_generate():
+    import torch.distributed as dist
+    from cassmantle_amd.parallel.dist import DistContext
+    from cassmantle_amd.parallel.rooms import GenJob, RankWorker, RoomSharding
+    from cassmantle_amd.pipeline import DiffusionImageGenerator
+    dev = torch.device("cuda:0")
+    assert not dist.is_initialized()
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        gen = DiffusionImageGenerator("tiny", device="cuda:0", use_graphs=True, seed=0)
+        done = []
+        w = RankWorker(DistContext(0, 1, 0, dev, "nccl"), gen, RoomSharding(["", "1"], 1),
+                       on_local_done=done.append)
+        jobs = [GenJob("", "a castle on a hill", 1), GenJob("1", "a river at night", 2), GenJob("", "a tower", 3)]
+        res = w.run_round(jobs, round_id=7)
+        assert done == [7]                               # published after the device work finished
+        assert w._comm is not None and w.last_gather_us is not None and w.last_gather_us > 0
+        ref = gen.generate([j.prompt for j in jobs], w.negative, [j.seed for j in jobs])
+        assert sorted(res) == [("", 0), ("", 2), ("1", 1)]
+        for i, j in enumerate(jobs):
+            im = res[(j.room, i)]
+            assert im.dtype == np.uint8 and im.shape == (16, 16, 3)
+            assert np.array_equal(im, ref[i]), i
+        # a second round reuses the comm stream and the graph-captured step
+        res2 = w.run_round(jobs[:1], round_id=8)
+        assert done == [7, 8] and np.array_equal(res2[("", 0)], ref[0])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_supervised_group_on_cuda0():
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    cfg = Config()
+    cfg.model.image_model = "tiny"
+    cfg.model.resolution = 16
+    cfg.model.steps = 4
+    rooms = ["", "1"]
+    sup = GroupSupervisor(cfg, ["cuda:0"], rooms, window_s=0.1, start_timeout_s=300)
+    try:
+        assert sup.backend == "nccl"
+        assert sup.wait_ready(300) and sup.live_devices() == ["cuda:0"]
+        f1, f2 = sup.submit("", ["a castle"], [1]), sup.submit("1", ["a river", "a tower"], [2, 3])
+        a, b = f1.result(timeout=300), f2.result(timeout=300)
+        st = sup.status()
+    finally:
+        sup.close()
+    assert len(a) == 1 and len(b) == 2
+    assert all(im.shape == (16, 16, 3) and im.dtype == np.uint8 for im in a + b)
+    assert st["rounds"] >= 1 and not st["retired"] and st["gather_us_p50"] is not None, st
