@@ -46,8 +46,6 @@ def parse():
     p.add_argument("--overlap", action="store_true", help="VAE decode on a side stream, overlapped with the next step's denoise")
     p.add_argument("--no-batch1", action="store_true", help="skip the batch-1 latency (s/image one room waits)")
     p.add_argument("--profile-steps", type=int, default=0)
-    p.add_argument("--branches", type=int, default=None,
-                   help="UNet batch branches on parallel streams (default: CASSMANTLE_UNET_BRANCHES / the pipeline's)")
     return p.parse_args()
 
 
@@ -207,8 +205,7 @@ def main() -> int:
     args.denoise_steps = args.denoise_steps or spec.steps
     args.scheduler = args.scheduler or spec.scheduler
     sd = StableDiffusion(spec, device=device, use_graphs=not (args.baseline or args.no_graphs),
-                         fp8_attention=args.fp8_attention, seed=0, overlap_decode=args.overlap,
-                         branches=args.branches)
+                         fp8_attention=args.fp8_attention, seed=0, overlap_decode=args.overlap)
     gen = SyntheticPromptGenerator(salt=rank)
     seeds_txt, styles = load_seeds(), load_styles()
     negative = "blurry, distorted, fake, abstract, negative"
@@ -340,7 +337,6 @@ def main() -> int:
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
             "batch1_s_per_image": b1,       # one room, one image, prompt -> host uint8
             "stage_overlap": sd.decode_stream is not None,
-            "unet_branches": sd.branches,
             "stage_mean_ms": stage_ms,      # device time per generation (incl. warmup)
             **score,
         }

@@ -148,7 +148,7 @@ class Conv2d(nn.Module):
             self.padded_weight(self.pad_in)
 
     def forward(self, x, residual=None, upsample=False, chan_bias=None, stats=None, out=None):
-        if out is not None:         # (the UNet's conv_out writing one branch's rows of eps)
+        if out is not None:         # (a caller-provided output buffer)
             w = self.padded_weight(x.shape[-1]) if x.shape[-1] > self.cin else self.weight
             return ops.conv2d(x, w, self.bias, self.stride, self.padding, residual=residual,
                               upsample=upsample, chan_bias=chan_bias, stats=stats, out=out)

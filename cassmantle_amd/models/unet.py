@@ -364,21 +364,17 @@ class UNet(nn.Module):
                 m.prepare()
         return self
 
-    def set_context(self, ctx: Optional[torch.Tensor], fp8: bool = False,
-                    splits: Optional[Sequence[Tuple[int, int]]] = None) -> None:
+    def set_context(self, ctx: Optional[torch.Tensor], fp8: bool = False) -> None:
         """Precompute all cross-attention K/V for a (constant) text context.  Buffers are kept
         per shape and refilled in place, so a captured denoise graph sees the new context.
-        ``fp8``: also pack each layer's K/V into the e4m3 image of the fp8 attention kernel, one
-        image per row range of ``splits`` (the batch branches :meth:`forward` runs with
-        ``kv_rows``; default: the whole batch)."""
+        ``fp8``: also pack each layer's K/V into the e4m3 image of the fp8 attention kernel."""
         if not getattr(self, "_fused", False):
             self.fuse_projections()
         ca = self.cross_attns()
         if ctx is None or self._kv_w is None:
             for m in ca:
-                m._kv = m._kv_all = None
+                m._kv = None
                 m._kv8 = None
-                m._kv8_rows = {}
             return
         key = (*ctx.shape[:-1], self._kv_w.shape[0])               # [B, L, sum 2C]
         buf = self._kv_bufs.get(key)
@@ -386,32 +382,18 @@ class UNet(nn.Module):
             self._kv_bufs[key] = buf = ops.linear(ctx, self._kv_w)
         else:
             ops.linear(ctx, self._kv_w, out=buf)                     # refilled in place
-        ranges = [tuple(r) for r in splits] if splits else [(0, buf.shape[0])]
         for m in ca:
-            m._kv_all = m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
-            m._kv8, m._kv8_rows = None, {}
+            m._kv = buf[:, :, m._kv_off:m._kv_off + m.to_kv.fout]
+            m._kv8 = None
             if fp8 and m.head_dim == 64 and ops._use_hip(buf):
-                # one e4m3 image per context shape and row range, like the bf16 K/V above: a
-                # denoise graph captured at another batch size keeps pointing at its own image,
-                # which is refilled in place and never freed (a single shared image
-                # was reallocated on a batch-size change under a live graph)
+                # one e4m3 image per context shape, like the bf16 K/V above: a denoise graph
+                # captured at another batch size keeps pointing at its own image, which is
+                # refilled in place and never freed (a single shared image was
+                # reallocated on a batch-size change under a live graph)
                 bufs8 = m.__dict__.setdefault("_kv8_bufs", {})
-                for r0, r1 in ranges:
-                    kv = m._kv_all[r0:r1].view(r1 - r0, buf.shape[1], 2, m.heads, m.head_dim)
-                    k8 = (key, str(buf.device), r0, r1)
-                    bufs8[k8] = ops.pack_kv_fp8(kv[:, :, 0], kv[:, :, 1], out=bufs8.get(k8))
-                    m._kv8_rows[(r0, r1)] = bufs8[k8]
-                m._kv8 = m._kv8_rows.get((0, buf.shape[0]))
-
-    def _select_kv_rows(self, rows: Optional[Tuple[int, int]]) -> None:
-        """Point every cross-attention at rows [r0, r1) of the context K/V (a batch branch)."""
-        for m in self.cross_attns():
-            full = getattr(m, "_kv_all", None)
-            if full is None:
-                continue
-            r0, r1 = rows if rows is not None else (0, full.shape[0])
-            m._kv = full[r0:r1]
-            m._kv8 = getattr(m, "_kv8_rows", {}).get((r0, r1))
+                kv = m._kv.view(buf.shape[0], buf.shape[1], 2, m.heads, m.head_dim)
+                k8 = (key, str(buf.device))
+                bufs8[k8] = m._kv8 = ops.pack_kv_fp8(kv[:, :, 0], kv[:, :, 1], out=bufs8.get(k8))
 
     def time_table(self, tsteps: torch.Tensor, nb: int, added: Optional[dict] = None,
                    t_rep: Optional[torch.Tensor] = None, rep_ids: Optional[torch.Tensor] = None):
@@ -439,15 +421,12 @@ class UNet(nn.Module):
 
     def forward(self, x: torch.Tensor, t: Optional[torch.Tensor], ctx: torch.Tensor,
                 added: Optional[dict] = None, fp8: bool = False, time_cond=None,
-                kv_rows: Optional[Tuple[int, int]] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x [B, H, W, 4] NHWC, t [B] (float), ctx [B, 77, D] -> eps [B, H, W, 4].
         ``time_cond``: (SiLU(temb) [B, D], time biases [B, sum Cout]) rows of :meth:`time_table`
-        (then ``t`` / ``added`` are not used for the time embedding).  ``kv_rows``: this call is
-        rows [r0, r1) of the batch :meth:`set_context` was given (a batch branch: the context
-        K/V rows and the GroupNorm statistics slab are its own).  ``out``: eps buffer to write."""
+        (then ``t`` / ``added`` are not used for the time embedding).  ``out``: eps buffer to write."""
         if not getattr(self, "_fused", False):
             self.fuse_projections()
-        self._select_kv_rows(kv_rows)
         if time_cond is not None:
             temb, tb = time_cond
         else:
@@ -456,7 +435,7 @@ class UNet(nn.Module):
         # every producer of a GroupNorm input (conv_in, ResNet conv1/conv2, transformer
         # proj_out, down/up-sample convs) accumulates the output statistics in its epilogue,
         # so the 61 GroupNorms of a step run their apply pass only
-        ar = self._arena.begin((tuple(x.shape), kv_rows), x)
+        ar = self._arena.begin(tuple(x.shape), x)
         B = x.shape[0]
         hs = ar.take(B, self.conv_in.cout)
         h = self.conv_in(x, stats=hs)

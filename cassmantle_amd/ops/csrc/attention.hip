@@ -40,17 +40,9 @@ struct AttnGeom {
 // DB: K/V double-buffered in LDS, so the next tile is stored into the other buffer while this
 // one is read and each tile needs ONE barrier (single buffer: one before the store -- everyone
 // is done reading -- and one after it)
-// PIPE (implies 3 K/V buffers): software-pipelined tiles -- the QK^T MFMAs of tile t + 1 are
-// issued before the softmax of tile t, so the matrix pipe works while the VALU runs the exps;
-// tiles are staged two ahead
-// STAG (implies 3 K/V buffers, tiles staged two ahead): two barriers per tile -- after the
-// QK^T + softmax half and after the P.V half -- with waves NW/2.. one barrier behind, so on every
-// SIMD one wave's softmax VALU runs beside its partner's P.V MFMAs instead of both waves of a SIMD
-// doing the same half at once (the per-tile barrier of the DB loop keeps them in lock-step).
-// Hazards: tile t+2 is stored during the P.V half of t into the buffer of t-1, whose last reader
-// (a late wave's P.V of t-1) passed its barrier before any early wave starts the P.V half of t;
-// an early wave reads tile t+2 after the late waves' P.V-half barrier of t+1 > their stores.
-template <int DQK, int DO, int NW, bool DB, bool PIPE = false, bool STAG = false>
+// (Measured and removed in round 4, kept in git history: software-pipelined tiles on 3 buffers,
+// profiles/r2_attn_pipe_ab.txt; staggered wave halves, profiles/r3_attn_stag_ab.txt.)
+template <int DQK, int DO, int NW, bool DB>
 // min blocks 8 / NW caps the kernel at 256 registers: the compiler then keeps the MFMA
 // accumulators in VGPRs, where the softmax reads and writes them (with a 512-register budget it
 // chose AGPRs and paid a v_accvgpr_read + write per score per pass: ~144 of ~300 VALU per tile)
@@ -183,159 +175,17 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     gload(0);
     lstore(0);
   }
-  const bool late = STAG && wave >= NW / 2;
-  if constexpr (STAG) {
-    if (ntiles > 1) {
-      gload(1);
-      lstore(BUF);
-    }
-  }
   __syncthreads();
-  if constexpr (STAG) {
-    if (late) __builtin_amdgcn_s_barrier();
-  }
 
   // tr-read lane geometry (T10): group g = lane>>4, i = lane&15 -> row q' = i>>2, col 4*(i&3)
   const int tg = lane >> 4, ti = lane & 15;
   const int tr_row = 4 * (tg >> 1) + (ti >> 2);
   const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
 
-  if constexpr (PIPE) {
-    constexpr float RESCALE_THR = 8.f;
-    // S^T of the tile staged at buffer offset bk (two 32-key accumulators), relative to m_run
-    auto qk = [&](f32x16_t (&sa)[2], int bk) {
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sa[hf][r] = MF ? 0.f : -m_run;
-        const uint16_t* krow = Ks + bk + (hf * 32 + ql) * G::KSTR + 8 * hlf;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
-          sa[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sa[hf], 0, 0, 0);
-        }
-      }
-    };
-    // softmax of tile t (scores sc) and O^T += V^T P^T from buffer offset bv; a rescale also
-    // shifts the next tile's scores sn (already computed against the old reference max)
-    auto soft_pv = [&](f32x16_t (&sc)[2], f32x16_t (&sn)[2], bool have_next, int bv, int t) {
-      const int kbase = t * KT;
-      if ((kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0)) {
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kbase + hf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hlf;
-            if (key >= nk || (a.causal && key > q)) sc[hf][r] = -INFINITY;
-          }
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[hf][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
-        asm volatile("" ::: "memory");
-        float delta = (t == 0) ? mx : fmaxf(mx, 0.f);
-        if (!(delta > -1e30f)) delta = 0.f;
-        if constexpr (MF) {
-          const float mn = (float)(__bf16)(m_run + delta);
-          delta = mn - m_run;
-          m_run = mn;
-          qf[2][0] = hlf ? (__bf16)(-m_run) : qf[2][0];
-        } else {
-          m_run += delta;
-        }
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
-        l_run *= alpha;
-#pragma unroll
-        for (int i = 0; i < NDC; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sc[hf][r] -= delta;
-        if (have_next) {
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sn[hf][r] -= delta;
-        }
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sc[hf][r]);
-          sc[hf][r] = pv;
-          if constexpr (!ones) rs += pv;
-        }
-      if constexpr (!ones) {
-        rs += __shfl_xor(rs, 32, 64);
-        l_run += rs;
-      }
-      bf16x8_t pf[4];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          uint4 u;
-          u.x = pack2(sc[hf][8 * s2 + 0], sc[hf][8 * s2 + 1]);
-          u.y = pack2(sc[hf][8 * s2 + 2], sc[hf][8 * s2 + 3]);
-          u.z = pack2(sc[hf][8 * s2 + 4], sc[hf][8 * s2 + 5]);
-          u.w = pack2(sc[hf][8 * s2 + 6], sc[hf][8 * s2 + 7]);
-          pf[2 * hf + s2] = as_bf16x8(u);
-        }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-#pragma unroll
-        for (int dc = 0; dc < NDC; ++dc) {
-          const uint16_t* base = Vs + bv + (16 * kk + tr_row) * G::VSTR + 32 * dc + tr_col;
-          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(base));
-          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4_t*)(base + 8 * G::VSTR));
-          typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-          s16x8_t vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          oacc[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv), pf[kk], oacc[dc], 0, 0, 0);
-        }
-      }
-    };
-    // tile t lives at buffer offset ((t % 3) * BUF); tile t + 2 is stored into the buffer of
-    // tile t - 1, whose K (read in tile t - 2) and V (read in tile t - 1) are done before the
-    // barrier that ended tile t - 1
-    if (ntiles > 1) {
-      gload(1);
-      lstore(BUF);
-    }
-    __syncthreads();
-    f32x16_t s0[2], s1[2];
-    if (ntiles > 0) qk(s0, 0);
-    int bc = 0;
-    auto step = [&](f32x16_t (&sc)[2], f32x16_t (&sn)[2], int t) {
-      const bool more = t + 1 < ntiles, more2 = t + 2 < ntiles;
-      const int bn = bc == 2 * BUF ? 0 : bc + BUF;
-      const int bs = bn == 2 * BUF ? 0 : bn + BUF;
-      if (more2) gload(t + 2);
-      if (more) qk(sn, bn);
-      soft_pv(sc, sn, more, bc, t);
-      if (more2) lstore(bs);
-      __syncthreads();
-      bc = bn;
-    };
-    for (int t = 0; t < ntiles; t += 2) {
-      step(s0, s1, t);
-      if (t + 1 >= ntiles) break;
-      step(s1, s0, t + 1);
-    }
-  } else {
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
-    const bool ahead = STAG ? t + 2 < ntiles : more;      // a tile is staged during this one
-    if (ahead) gload(STAG ? t + 2 : t + 1);
-    const int bo = STAG ? (t % 3) * BUF : (DB ? (t & 1) * BUF : 0);   // this tile's buffer
+    if (more) gload(t + 1);                          // staged during this tile
+    const int bo = DB ? (t & 1) * BUF : 0;           // this tile's buffer
 
     // ---- S^T = K Q^T for 64 keys (two 32-key accumulators)
     f32x16_t sacc[2];
@@ -438,12 +288,6 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
         pf[2 * hf + s] = as_bf16x8(u);
       }
 
-    if constexpr (STAG) {
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-    }
     // ---- O^T += V^T P^T
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -461,13 +305,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
       }
     }
 
-    if constexpr (STAG) {
-      __builtin_amdgcn_s_setprio(0);
-      if (ahead) lstore(((t + 2) % 3) * BUF);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else if constexpr (DB) {
+    if constexpr (DB) {
       // the other buffer was last read in tile t - 1, which every wave finished before the
       // previous barrier
       if (more) lstore(BUF - bo);
@@ -479,10 +317,6 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
         __syncthreads();
       }
     }
-  }
-  if constexpr (STAG) {
-    if (!late) __builtin_amdgcn_s_barrier();   // re-align the two halves
-  }
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l
@@ -521,53 +355,18 @@ void launch_t(const AttnArgs& a, hipStream_t s) {
   constexpr int QB = 32 * NW;
   int nqb = (a.Nq + QB - 1) / QB;
   dim3 grid(nqb * a.H * a.B);
-  // CASSMANTLE_ATTN_DB=0|1: single / double-buffered K/V (A/B knob; double by default: level-1
-  // self-attention 247 -> 240 us, 568.7 -> 566.7 ms/step same box x3, profiles/r2_attn_db_ab.txt)
-  static const int db = [] { const char* e = getenv("CASSMANTLE_ATTN_DB"); return e ? atoi(e) : 1; }();
-  if constexpr (NW >= 4 && DO <= 96) {   // (the larger head dims spill in this variant)
-    if (db == 3) {
-      // CASSMANTLE_ATTN_DB=3: staggered waves on 3 K/V buffers (attn_fwd_kernel STAG)
-      auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true, false, true>;
-      if constexpr (3 * G::LDS_BYTES > 65536) {
-        static const bool once = [&] {
-          (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * G::LDS_BYTES);
-          return true;
-        }();
-        (void)once;
-      }
-      hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 3 * G::LDS_BYTES, s, a);
-      return;
-    }
+  // K/V double-buffered in LDS (level-1 self-attention 247 -> 240 us, 568.7 -> 566.7 ms/step
+  // same box x3, profiles/r2_attn_db_ab.txt; the single-buffer variant was removed in round 4)
+  auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true>;
+  if constexpr (2 * G::LDS_BYTES > 65536) {
+    // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
+    static const bool once = [&] {
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G::LDS_BYTES);
+      return true;
+    }();
+    (void)once;
   }
-  if constexpr (DQK <= 64) {
-    if (db == 2) {
-    // CASSMANTLE_ATTN_DB=2: software-pipelined tiles on 3 K/V buffers (head dims <= 64: the
-    // second score accumulator spills registers at the larger ones)
-    auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true, true>;
-    if constexpr (3 * G::LDS_BYTES > 65536) {
-      static const bool once = [&] {
-        (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * G::LDS_BYTES);
-        return true;
-      }();
-      (void)once;
-    }
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 3 * G::LDS_BYTES, s, a);
-    return;
-    }
-  }
-  if (db) {
-    auto* kfn = &attn_fwd_kernel<DQK, DO, NW, true>;
-    if constexpr (2 * G::LDS_BYTES > 65536) {
-      // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
-      static const bool once = [&] {
-        (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G::LDS_BYTES);
-        return true;
-      }();
-      (void)once;
-    }
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 2 * G::LDS_BYTES, s, a);
-  } else
-    hipLaunchKernelGGL((attn_fwd_kernel<DQK, DO, NW, false>), grid, dim3(64 * NW), G::LDS_BYTES, s, a);
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), 2 * G::LDS_BYTES, s, a);
 }
 
 template <int DQK, int DO>

@@ -30,32 +30,35 @@ constexpr int BK = 64;
 //   5: 256x160 (4x2, wave 64x80)   6: 256x128 (4x2, wave 64x64)
 // 8-wave ping-pong kernel (gemm_pp.h; 1 block per CU, 4 phases per k-tile, counted vmcnt):
 //   7: 256x256   8: 256x160   9: 256x128   10: 128x256
-// deep LDS ring (gemm_impl.h STAGES 4-5, one block per CU; buffer-resource modes, bf16 out):
-//   11: 128x160 4w S4   12: 128x128 4w S4 (also gated)   13: 128x64 4w S5   14: 128x160 8w S4
+// deep LDS ring (gemm_impl.h STAGES 3-5, one block per CU; buffer-resource modes, bf16 out):
+//   12: 128x128 4w S4 (also gated)   13: 128x64 4w S5   14: 128x160 8w S4
 //   15: A-in-registers short-K kernel (gemm_areg.hip: K = 320 / 640, W streamed in chunks)
 //   16: 128x80 4w (4x1, wave 32x80) S4: M = 2048 x N = 1280 is exactly 256 tiles, one per CU
 //       (the 128x64 tile's 320 blocks ran as 1.25 rounds; the deep rings are one block per CU)
-//   17 / 18 / 19: 128x64 / 128x128 / 128x160 4w, 2 stages staged through registers (buffer
-//       loads + ds_write instead of LDS-DMA: no DMA issue cost on the small latency-bound tiles)
 //   20: ping-pong 128x160 (4x2 waves, wave 32x80): twice the blocks of 256x160 without split-K
 //       (M = 8192 x N = 640: 256 tiles)
 //   21: ping-pong 128x128 (4x2 waves, wave 32x64, 64 KiB LDS: 2 blocks per CU)
-//   22 / 23: ping-pong 128x64 / 256x64 (4x2 waves, 48 / 80 KiB LDS)
-//   24 / 25: halo-staged 3x3 conv 256x160 / 128x160 (gemm_halo.h: one halo tile per 64-channel
-//       chunk serves all 9 taps; half the LDS-DMA bytes per k-tile of the CONV 2 path)
-//   28: 16-wave 128x64 (8x2 waves, wave 16x32, 3 stages): 16 waves issuing the DMA (48 B/cycle)
-//   29 / 30: 8-wave 128x128 (4x2 waves, wave 32x64) / 256x80 (8x1 waves, wave 32x80), 3 stages
+//   22: ping-pong 128x64 (4x2 waves, 48 KiB LDS)
 //   26 / 27: 8-wave 128x80 (8x1 waves, wave 16x80, 4-stage ring) / 128x64 (4x2 waves, 3 stages):
 //       the small-grid tiles with twice the waves issuing LDS-DMA.  A CU's LDS-DMA fill rate is
 //       set by the number of waves issuing it, not by the bytes in flight (4 waves: 22 B/cycle
 //       on the GEMM row pattern at any ring depth, 8 waves: 37; profiles/r3_lds_fill_probe.jsonl)
+// Removed in round 4 (measured, picked by no shape of the SD-1.5 / SDXL census; results kept in
+// profiles/ and in git history): 11 (128x160 4w S4), 17-19 (register-staged 4-wave tiles,
+// profiles/r2_regstage_ab.txt), 23 (ping-pong 256x64), 24/25 (halo-staged 3x3 conv,
+// profiles/r3_bench_halo.jsonl), 28 (16-wave 128x64, profiles/r3_probe_16wave.jsonl), 29/30 (8-wave
+// 128x128 / 256x80 and the gated 128x128, profiles/r3_tune_8wave_b_ab.txt,
+// profiles/r3_tune_8wave_gated.txt).  Their indices stay reserved so table keys keep their meaning.
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
 constexpr int kNumTiles = 31;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
-constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22 || c == 23; }
-constexpr bool is_halo_cfg(int c) { return c == 24 || c == 25; }
+constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22; }
+// configs with a kernel behind them (the reserved indices above have none)
+constexpr bool is_live_cfg(int c) {
+  return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 22) || c == 26 || c == 27;
+}
 constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
 constexpr int kFirstDeep = 11;
@@ -249,9 +252,8 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     }
     // a table entry is only taken if the kernel family can run this call (same checks as a
     // forced config), so a stale table never selects an unsupported path
-    const bool elig = tp.cfg < kFirstPP ||
-                      (is_pp_cfg(tp.cfg) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p)
-                                                       : is_halo_cfg(tp.cfg) ? gemm_halo_ok(p, tp.cfg) : deep_ok(p)));
+    const bool elig = is_live_cfg(tp.cfg) &&
+                      (tp.cfg < kFirstPP || (is_pp_cfg(tp.cfg) ? pp_ok(p) : (tp.cfg == kAreg ? gemm_areg_ok(p) : deep_ok(p))));
     if (have && elig) return tp;
   }
   static const int use_big = env_int("CASSMANTLE_GEMM_8WAVE", 0);
@@ -265,17 +267,11 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
   const bool deep_elig = deep_ok(p);
   if (force_cfg == kAreg) {
     if (gemm_areg_ok(p)) return GemmPlan{kAreg, 1};
-  } else if (is_halo_cfg(force_cfg)) {
-    if (gemm_halo_ok(p, force_cfg)) {
-      const int nch = p.Cin / 64;
-      const int sp = force_split > 0 ? force_split : 1;
-      if (sp <= nch && sp <= GEMM_MAX_SPLIT && (sp == 1 || p.N % 4 == 0)) return GemmPlan{force_cfg, sp};
-    }
-  } else if (force_cfg >= 0 && force_cfg < kNumTiles && ((force_cfg == 4) == (p.N <= 16)) &&
+  } else if (force_cfg >= 0 && is_live_cfg(force_cfg) && ((force_cfg == 4) == (p.N <= 16)) &&
       (force_cfg < kFirstPP || (is_pp_cfg(force_cfg) ? pp_elig : deep_elig))) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
-      else if (force_cfg >= kFirstDeep) best.cfg = force_cfg == 29 ? 29 : 12;   // the deep-ring gated tiles (4 / 8 waves)
+      else if (force_cfg >= kFirstDeep) best.cfg = 12;    // the deep-ring gated tile
       else if (force_cfg >= kFirstPP) best.cfg = force_cfg == 8 ? 8 : 9;   // the ping-pong gated tiles
       return best;
     }
@@ -336,10 +332,6 @@ void launch_gemm(const GemmArgs& p, float* ws, hipStream_t s) {
     return;
   }
   const bool buf = buf_ok(p);
-  if (is_halo_cfg(p.cfg) && gemm_halo_ok(p, p.cfg)) {
-    gemm_halo_launch(p, ws, s);
-    return;
-  }
   if (p.cfg == kAreg && gemm_areg_ok(p)) {
     launch_gemm_areg(p, s);
     return;

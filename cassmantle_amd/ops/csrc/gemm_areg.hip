@@ -483,14 +483,9 @@ bool gemm_areg_ok(const GemmArgs& p) {
     if (p.gn_groups <= 0 || p.K % p.gn_groups || p.gn_gamma == nullptr || p.gn_beta == nullptr) return false;
   }
   if (p.ln_wsum && !(p.ln_eps > 0.f)) return false;
-  // K = 1280 (16 rows per wave, 160 A registers, 16-row W chunks on a 2-deep ring): the
-  // latency-bound level-3 projections (M = 2048); opt-in while it is being measured
-  static const bool k1280 = [] { const char* e = getenv("CASSMANTLE_AREG_K1280"); return e && e[0] == '1'; }();
-  const bool is1280 = p.K == 1280 && k1280;
-  if (!(p.K == 320 || p.K == 640 || is1280) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
+  if (!(p.K == 320 || p.K == 640) || p.lda % 8 || p.ldc % 8 || p.N % 8) return false;
   const bool gated = is_gated(p.act);
-  if (is1280 && gated) return false;
-  const int bnc = p.K == 320 ? 64 : (p.K == 640 ? 32 : 16);
+  const int bnc = p.K == 320 ? 64 : 32;
   if ((gated ? 2 * p.N : p.N) % bnc) return false;
   if (gated && p.stats) return false;
   if (p.stats && (p.stats_hw % 64 != 0)) return false;
@@ -501,47 +496,21 @@ bool gemm_areg_ok(const GemmArgs& p) {
   return ((long long)(p.Nw - 1) * (p.ldw ? p.ldw : p.K) + p.K) * 2 <= lim;
 }
 
-static int areg_variant() {
-  static const int v = [] {
-    const char* e = getenv("CASSMANTLE_AREG_V");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
-// Instantiations (measured on the SD-1.5 batch-8 level-1/2 shapes, profiles/r2_areg_variants.jsonl):
-//   v0: 40 KiB chunks, 1 block / CU               v1: 20 KiB chunks, 2 blocks / CU
-//   v2: v1 with 64 rows per wave for gated K = 320 (each LDS W fragment feeds 4 MFMAs, not 2)
-//   v3: v2, and the K = 640 tiles on a 2-deep ring (80 KiB: 2 blocks per CU instead of 1)
-//   v4: v3, and the non-gated K = 320 tiles on a 2-deep ring (40 KiB: 3 blocks per CU)
-// default (-1): v3 (K = 640 ring 2: 585 -> 580 ms/step same box x3, profiles/r2_areg_ring2_ab.txt)
+// Tiles (measured on the SD-1.5 batch-8 level-1/2 shapes, profiles/r2_areg_variants.jsonl,
+// profiles/r2_areg_ring2_ab.txt): K = 320 on 64-row W chunks through a 3-deep ring (2 blocks per
+// CU), 64 A rows per wave for the gated tiles (each LDS W fragment feeds 4 MFMAs); K = 640 on
+// 32-row chunks through a 2-deep ring (80 KiB: 2 blocks per CU).  The measured-slower variants
+// (1 block per CU, 3 blocks per CU, 16-row chunks, a K = 1280 tile) were removed in round 4
+// (profiles/r2_areg_v4_ab.txt, profiles/r2_areg_k1280.txt; git history).
 template <bool LNK>
 void launch_gemm_areg_t(const GemmArgs& p, hipStream_t s) {
   const bool gated = is_gated(p.act);
-  int v = areg_variant();
-  if (v < 0) v = 3;
-  if (p.K == 1280) {
-    launch_areg_t<40, 1, 2, 1, false, LNK>(p, s);
-    return;
-  }
   if (p.K == 320) {
-    if (v >= 2 && gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
-    else if (v == 4 && !gated) launch_areg_t<10, 2, 2, 2, false, LNK>(p, s);   // 40 KiB: 3 blocks per CU
-    else if (v >= 1) gated ? launch_areg_t<10, 2, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
-    else gated ? launch_areg_t<10, 4, 3, 2, true, LNK>(p, s) : launch_areg_t<10, 4, 3, 2, false, LNK>(p, s);
+    if (gated) launch_areg_t<10, 2, 3, 4, true, LNK>(p, s);   // RW = 4 spills without the gate pairing
+    else launch_areg_t<10, 2, 3, 2, false, LNK>(p, s);
   } else {
-    // CASSMANTLE_AREG_LNK16=1: the 16-row-chunk variant for the in-kernel LayerNorm too (it gave
-    // run-to-run last-bit differences with the builtin permlane swaps; see sum_row_groups)
-    static const bool lnk16 = [] { const char* e = getenv("CASSMANTLE_AREG_LNK16"); return e && e[0] == '1'; }();
-    if (LNK && lnk16 && !gated) {
-      launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
-      return;
-    }
-    // v3: 2-deep ring (80 KiB, 2 blocks per CU) for the 32-row chunks
-    if (v >= 3) gated ? launch_areg_t<20, 2, 2, 2, true, LNK>(p, s) : launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
-    else if (gated) launch_areg_t<20, 2, 3, 2, true, LNK>(p, s);
-    else if (v >= 1 && !LNK) launch_areg_t<20, 1, 3, 2, false, LNK>(p, s);
-    else launch_areg_t<20, 2, 3, 2, false, LNK>(p, s);
+    if (gated) launch_areg_t<20, 2, 2, 2, true, LNK>(p, s);
+    else launch_areg_t<20, 2, 2, 2, false, LNK>(p, s);
   }
 }
 

@@ -446,11 +446,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
 // keep STAGES-2 k-tiles of DMA in flight across every barrier: the short-K / small-grid UNet
 // GEMMs (K = 320..1280, <= 2 tiles per CU) are bound by the per-k-tile DMA latency, not by
 // MFMA, and a 2-stage loop exposes that latency once per k-tile.
-// REG (BUF only, 2 stages): k-tiles staged through REGISTERS -- buffer loads with the same
-// resources / offsets as the LDS-DMA path into VGPRs, written to the other LDS buffer after the
-// MFMAs of the current tile, one barrier per k-tile.  An LDS-DMA piece costs ~60-185 issue
-// cycles (MI355X_MICROARCH.md constants table), which bounds the small latency-bound tiles.
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, bool REG = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
 __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 && STAGES == 2) ? 2 : 1)
 gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -458,7 +454,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   constexpr int THREADS = 64 * NW;
   constexpr int RR = 8 * NW;               // rows covered by one DMA round (8 per wave)
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
-  static_assert(NW == 4 || NW == 8 || NW == 16, "4, 8 or 16 waves");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int TI = BN / WN / 16;         // n-subtiles per wave
   constexpr int TJ = BM / WM / 16;         // m-subtiles per wave
   static_assert(!GEGLU || (TI % 2 == 0), "geglu pairs");
@@ -737,67 +733,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
   if constexpr (CONV >= 2) tap_init(kt0);
 
-  if constexpr (REG) {
-    static_assert(BUF && STAGES == 2, "register staging: buffer-resource modes, 2 LDS buffers");
-    uint4 rst[AR + WR];
-    // the BUF stage() with buffer loads into registers instead of LDS-DMA
-    auto rload = [&](int kt) {
-      const int k0 = kt * BK;
-      int soffA = k0 * 2, tap = 0;
-      if constexpr (CONV == 2) {
-        soffA = ((t_ky * p.IW + t_kx) * p.Cin + t_ci) * 2;
-        tap = t_ky * p.ksize + t_kx;
-      }
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        int vo = a_vo[i];
-        __amdgpu_buffer_rsrc_t rs = rsA;
-        int so = soffA;
-        if constexpr (CONV == 0) {
-          if (p.A2 != nullptr && k0 >= p.ka) { rs = rsA2; vo = a_vo2[i]; so = (k0 - p.ka) * 2; }
-        } else {
-          vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
-        }
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
-        rst[i] = __builtin_bit_cast(uint4, v);
-      }
-#pragma unroll
-      for (int i = 0; i < WR; ++i) {
-        if (RR * i + 8 * wave < BN) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsW, w_vo[i], k0 * 2, 0);
-          rst[AR + i] = __builtin_bit_cast(uint4, v);
-        }
-      }
-      if constexpr (CONV >= 2) tap_next();
-    };
-    // lane L of a DMA piece lands at uint4 L of the piece's 1 KiB: the same LDS image
-    auto rcommit = [&](int buf) {
-      uint4* As = smem + buf * TILE;
-      uint4* Ws = As + BM * 8;
-#pragma unroll
-      for (int i = 0; i < AR; ++i) As[(RR * i + 8 * wave) * 8 + lane] = rst[i];
-#pragma unroll
-      for (int i = 0; i < WR; ++i)
-        if (RR * i + 8 * wave < BN) Ws[(RR * i + 8 * wave) * 8 + lane] = rst[AR + i];
-    };
-    if (nk > 0) {
-      rload(kt0);
-      rcommit(0);
-    }
-    __syncthreads();
-    for (int t = 0; t < nk; t += 2) {
-      // buffer 1 was last read in tile t - 1, finished by every wave before the last barrier
-      if (t + 1 < nk) rload(kt0 + t + 1);
-      compute(0);
-      if (t + 1 < nk) rcommit(1);
-      __syncthreads();
-      if (t + 1 >= nk) break;
-      if (t + 2 < nk) rload(kt0 + t + 2);
-      compute(1);
-      if (t + 2 < nk) rcommit(0);
-      __syncthreads();
-    }
-  } else if constexpr (STAGES == 2) {
+  if constexpr (STAGES == 2) {
     if (nk > 0) stage(kt0, 0);
     __syncthreads();                       // drains the DMA (vmcnt(0)) and publishes the tile
     // unrolled by two so the LDS buffer of every stage/compute is a compile-time offset
@@ -969,16 +905,7 @@ void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s
   }
 }
 
-// CASSMANTLE_GEMM_STAGES (A/B knob for the microbenchmark), read once
-inline int stages_pref() {
-  static const int v = [] {
-    const char* e = getenv("CASSMANTLE_GEMM_STAGES");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, bool REG = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
 void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -989,7 +916,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = lds_stage > lds_epi ? lds_stage : lds_epi;
   // (the kernel is named once, outside any lambda: a kernel template referenced only from a
   // lambda inside this function template was left uninstantiated by hipcc)
-  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, REG>;
+  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
     // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
@@ -1008,15 +935,9 @@ void launch_st(const GemmArgs& p, float* ws, hipStream_t s) {
   if constexpr (WM * WN == 8) {
     launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3, BUF>(p, ws, s);
   } else {
-  // STAGES=3 (counted vmcnt, one block/CU) measured 1.3-1.7x SLOWER than 2 stages at 2
-  // blocks/CU on every SD shape (profiles/r1_ops_stages_ab.txt); define CASSMANTLE_GEMM_3STAGE
-  // to compile it for experiments.
-#ifdef CASSMANTLE_GEMM_3STAGE
-  if constexpr (BN % 32 == 0 && !BUF) {
-    if (stages_pref() == 3) return launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 3, false>(p, ws, s);
-  }
-#endif
-  launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2, BUF>(p, ws, s);
+    // (4-wave tiles: STAGES=3 at one block/CU measured 1.3-1.7x SLOWER than 2 stages at 2
+    // blocks/CU on every SD shape, profiles/r1_ops_stages_ab.txt)
+    launch_t<BM, BN, WM, WN, CONV, GEGLU, OUTF32, 2, BUF>(p, ws, s);
   }
 }
 
@@ -1025,19 +946,12 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
   // deep-ring tiles (buffer-resource modes, bf16 out): one block per CU, STAGES-2 k-tiles ahead
   if constexpr (BUF && !OUTF32) {
     switch (p.cfg) {
-      case 11: return launch_t<128, 160, 2, 2, CONV, false, false, 4, true>(p, ws, s);
       case 12: return launch_t<128, 128, 2, 2, CONV, false, false, 4, true>(p, ws, s);
       case 13: return launch_t<128, 64, 2, 2, CONV, false, false, 5, true>(p, ws, s);
       case 14: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true>(p, ws, s);
       case 16: return launch_t<128, 80, 4, 1, CONV, false, false, 4, true>(p, ws, s);
-      case 17: return launch_t<128, 64, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
-      case 18: return launch_t<128, 128, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
-      case 19: return launch_t<128, 160, 2, 2, CONV, false, false, 2, true, true>(p, ws, s);
       case 26: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true>(p, ws, s);
       case 27: return launch_t<128, 64, 4, 2, CONV, false, false, 3, true>(p, ws, s);
-      case 28: return launch_t<128, 64, 8, 2, CONV, false, false, 3, true>(p, ws, s);
-      case 29: return launch_t<128, 128, 4, 2, CONV, false, false, 3, true>(p, ws, s);
-      case 30: return launch_t<256, 80, 8, 1, CONV, false, false, 3, true>(p, ws, s);
       default: break;
     }
   }
@@ -1057,7 +971,6 @@ void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
   if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) {
     if constexpr (BUF) {
       if (p.cfg == 12) return launch_t<128, 128, 2, 2, CONV, true, false, 4, true>(p, ws, s);
-      if (p.cfg == 29) return launch_t<128, 128, 4, 2, CONV, true, false, 3, true>(p, ws, s);   // 8-wave gated
     }
     if (p.cfg == 6) launch_st<256, 128, 4, 2, CONV, true, false, BUF>(p, ws, s);
     else launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);

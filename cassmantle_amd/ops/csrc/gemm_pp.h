@@ -510,11 +510,9 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   const int split = (ws != nullptr && p.split > 1) ? p.split : 1;
   dim3 grid(nN * nM, split, p.batch);
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
-  // CASSMANTLE_PP_SCHED=0|1|2 picks the mainloop schedule (gemm_pp_kernel SCHED), A/B knob
-  static const int sched = [] { const char* e = getenv("CASSMANTLE_PP_SCHED"); return e ? atoi(e) : 2; }();
-  auto* kfn = sched >= 2 ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>
-              : sched == 1 ? &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 1>
-                           : &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 0>;
+  // the two-phase schedule (SCHED 2; 593 -> 573 ms/step, commit 88fbe5c).  SCHED 0 / 1 are no
+  // longer instantiated in the library (tools/ppdiag.hip still builds them for diagnostics)
+  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -543,7 +541,6 @@ void launch_pp_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
     case 20: launch_pp<128, 160, 4, 2, CONV, false>(p, ws, s); break;
     case 21: launch_pp<128, 128, 4, 2, CONV, false>(p, ws, s); break;
     case 22: launch_pp<128, 64, 4, 2, CONV, false>(p, ws, s); break;
-    case 23: launch_pp<256, 64, 4, 2, CONV, false>(p, ws, s); break;
     default: launch_pp<256, 256, 4, 2, CONV, false>(p, ws, s); break;
   }
 }

@@ -133,9 +133,6 @@ void launch_layer_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
 // per-row (mean, rstd) float2 of [rows][D] (LayerNorm statistics for a folded-LN GEMM)
 // A-in-registers short-K GEMM (gemm_areg.hip): shapes it takes, and the launch
 bool gemm_areg_ok(const GemmArgs& p);
-// halo-staged 3x3 conv (gemm_halo.h): tile configs 24 / 25
-bool gemm_halo_ok(const GemmArgs& p, int cfg);
-void gemm_halo_launch(const GemmArgs& p, float* ws, hipStream_t s);
 void launch_gemm_areg(const GemmArgs& p, hipStream_t s);
 void launch_row_stats(const uint16_t* x, float* stats, long long rows, int D, float eps, hipStream_t s);
 // fused encoder input layer: y[r] = LN(word[ids[r]] + pos[r % seq] + add) (bf16, D % 8 == 0)

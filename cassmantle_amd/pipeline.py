@@ -63,12 +63,9 @@ _VAE_GRAPH = os.environ.get("CASSMANTLE_VAE_GRAPH", "0") == "1"
 # text encoders captured as a graph per batch shape (CLIPTextEncoder.encode(graphs=True));
 # opt-in (CASSMANTLE_TEXT_GRAPH=1): no measured gain (profiles/r3_fusions_ab.txt)
 _TEXT_GRAPH = os.environ.get("CASSMANTLE_TEXT_GRAPH", "0") == "1"
-# Batch branches of the UNet evaluation: the CFG batch (uncond rows | cond rows) runs as this many
-# independent row ranges, each on its own stream, forked and joined inside the captured step
-# graph.  A batch-8 SD-1.5 step leaves most of the chip idle in its latency-bound kernels (the
-# 16^2 / 8^2 levels, GroupNorm, split-K reduce, short attention); two concurrent half-batch
-# branches fill each other's gaps.
-_BRANCHES = int(os.environ.get("CASSMANTLE_UNET_BRANCHES", "1"))
+# (The CFG batch as concurrent row-range branches on parallel streams inside the captured step was
+# measured 7-13 % slower than one batch-8 stream, profiles/r3_unet_branches_ab.txt; removed in
+# round 4, kept in git history.)
 
 
 class _StepState:
@@ -98,7 +95,6 @@ class _StepState:
         if added is not None:
             self.tid_rep = added["time_ids"].detach().cpu().repeat(E, 1).to(device)
         self.z = torch.empty((B, h, w, 4), device=device, dtype=dtype)      # bf16 latents for the VAE
-        self.eps = torch.empty((nb, h, w, 4), device=device, dtype=dtype)   # branch outputs (rows)
         self.finite = torch.empty((16,), device=device, dtype=torch.uint8)[:1]   # set by finalize_latents
         self.step = ops.zero_(torch.empty((4,), device=device, dtype=torch.int32))[:1]
         self.added = None
@@ -141,7 +137,7 @@ class _StepState:
 class StableDiffusion:
     def __init__(self, spec: PipelineSpec, device=None, dtype=torch.bfloat16, seed: int = 0,
                  use_graphs: bool = True, fp8_attention: bool = False, overlap_decode: bool = False,
-                 stream: Optional["torch.cuda.Stream"] = None, branches: Optional[int] = None) -> None:
+                 stream: Optional["torch.cuda.Stream"] = None) -> None:
         self.spec = spec
         self.device = torch.device(device) if device is not None else default_device()
         self.dtype = dtype
@@ -170,11 +166,6 @@ class StableDiffusion:
         # replay by more than the 21 ms of encode + decode they hide
         self.decode_stream = (torch.cuda.Stream(device=self.device)
                               if self.device.type == "cuda" and overlap_decode else None)
-        # UNet batch branches (see _BRANCHES): streams of branches 1.. (branch 0 runs on the
-        # step's own stream); same priority as the generation stream
-        self.branches = max(1, _BRANCHES if branches is None else int(branches))
-        self.branch_streams = ([torch.cuda.Stream(device=self.device) for _ in range(self.branches - 1)]
-                               if self.device.type == "cuda" else [])
         # one generation at a time per pipeline: the per-shape step state (latents, K/V context
         # buffers, time table, captured graph) is shared, so concurrent callers (several rooms'
         # worker threads) must not interleave (serving batches rooms through
@@ -208,37 +199,10 @@ class StableDiffusion:
         return ctx, {"time_ids": tid, "text_embeds": pooled}
 
     # ------------------------------------------------------------------ denoise
-    def _branch_rows(self, nb: int):
-        """Row ranges of the UNet batch branches (None: one branch), contiguous and equal."""
-        n = self.branches
-        if n <= 1 or nb % n:
-            return None
-        k = nb // n
-        return [(i * k, (i + 1) * k) for i in range(n)]
-
     def _unet_step(self, st: _StepState) -> None:
         # this step's rows of the per-plan time tables (st.*_cur: filled for step 0 by load(),
         # then by the previous step's latent-step launch from the device step counter)
-        ranges = self._branch_rows(st.unet_in.shape[0])
-        if ranges is None:
-            eps = self.unet(st.unet_in, None, st.ctx, st.added, fp8=self.fp8, time_cond=(st.temb_cur, st.tb_cur))
-        else:
-            # fork: branch i > 0 on its own stream after everything already queued on the step's
-            # stream; each branch writes its rows of st.eps; join before the latent step
-            # (on the CPU the branches simply run one after another)
-            main = torch.cuda.current_stream(self.device) if self.branch_streams else None
-            for s in self.branch_streams[:len(ranges) - 1]:
-                s.wait_stream(main)
-            for i, (r0, r1) in reversed(list(enumerate(ranges))):
-                s = self.branch_streams[i - 1] if i and self.branch_streams else None
-                added = None if st.added is None else {k: v[r0:r1] for k, v in st.added.items()}
-                with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
-                    self.unet(st.unet_in[r0:r1], None, st.ctx[r0:r1], added, fp8=self.fp8,
-                              time_cond=(st.temb_cur[r0:r1], st.tb_cur[r0:r1]), kv_rows=(r0, r1),
-                              out=st.eps[r0:r1])
-            for s in self.branch_streams[:len(ranges) - 1]:
-                main.wait_stream(s)
-            eps = st.eps
+        eps = self.unet(st.unet_in, None, st.ctx, st.added, fp8=self.fp8, time_cond=(st.temb_cur, st.tb_cur))
         ops.latent_step(eps, st.x, st.hist, st.xs, st.coef, st.step, st.unet_in, st.cfg,
                         rows=[(st.temb_tab, st.temb_cur), (st.tb_tab, st.tb_cur)])
         ops.advance_step(st.step)
@@ -307,7 +271,7 @@ class StableDiffusion:
         self._last_state = st
         # cross-attention K/V of the (loop-invariant) text context: one GEMM per generation,
         # written into per-shape buffers that the captured step graph reads
-        self.unet.set_context(ctx, fp8=self.fp8, splits=self._branch_rows(ctx.shape[0]))
+        self.unet.set_context(ctx, fp8=self.fp8)
         # time embedding + every ResNet's time bias for all timesteps of the plan: one batched
         # MLP + GEMM per generation (in place, so a captured step graph reads the new values)
         added_t = dict(added, time_ids_rep=st.tid_rep) if added is not None and st.tid_rep is not None else added

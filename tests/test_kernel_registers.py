@@ -14,12 +14,7 @@ CSRC = os.path.join(ROOT, "cassmantle_amd", "ops", "csrc")
 HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
 
 # kernels that may spill (opt-in variants / knobs, documented where they are instantiated)
-ALLOWED = ("ILi256ELi256ELi4ELi2ELi2ELb0ELi1ELi0E",   # ping-pong SCHED 1 256x256 (knob, 16 B)
-           "ILi256ELi256ELi4ELi2ELi0ELb0ELi1ELi0E",
-           "gemm_areg_kernelILi20ELi2ELi2ELi2ELb0",    # K = 640 ring-2 tiles (28-36 B, measured, default)
-           "gemm_areg_kernelILi10ELi2ELi2ELi2ELb0",    # v4 knob
-           "attn_fwd_kernelILi128ELi128ELi4ELb1ELb0ELb1E", "attn_fwd_kernelILi160ELi160ELi8ELb1ELb0ELb1E",
-           "attn_fwd_kernelILi160ELi160ELi4ELb1ELb0ELb1E")   # staggered attention knob (not launched > d 96)
+ALLOWED = ("gemm_areg_kernelILi20ELi2ELi2ELi2ELb0",)    # K = 640 ring-2 tiles (28-36 B, measured, default)
 
 
 def _scratch(tu):

@@ -505,7 +505,7 @@ def test_latent_step_matches_reference(sched):
 
 
 # ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
-PP_CFGS = [7, 8, 9, 10, 11, 12, 13, 14, 16, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28, 29, 30]   # ping-pong (7-10, 20-23), deep-ring (11-14, 16, 8-wave 26/27/29/30, 16-wave 28), register-staged (17-19)
+PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 26, 27]   # ping-pong (7-10, 20-22), deep-ring (12-14, 16, 8-wave 26/27)
 
 
 @pytest.fixture
@@ -890,57 +890,6 @@ def test_qkv_epilogue_emits_fp8_kv(N, C, split):
     # one-ulp e4m3 differences in ~3 % of K/V move the output by fp8 noise (2.7 % at 256 keys)
     assert rel_err(o1, o2) < 0.05
     assert rel_err(o1, exp) < 0.12 and rel_err(o2, exp) < 0.12
-
-
-# halo-staged 3x3 conv (gemm_halo.h, forced tile configs 24 = 256x160, 25 = 128x160): whole
-# output rows per tile, one halo per 64-channel chunk, the 9 taps read at row offsets
-@pytest.mark.parametrize("cfg", [24, 25])
-@pytest.mark.parametrize("B,H,W,Cin,Cout,split", [
-    (2, 64, 64, 320, 320, 1),       # SD-1.5 level-1 conv (7-round halo at 256 rows)
-    (1, 32, 32, 128, 192, 1),       # partial N tile
-    (2, 16, 16, 64, 64, 1),         # one image per 256-row tile, N < BN
-    (2, 32, 32, 256, 320, 2),       # split-K over channel chunks
-    (1, 16, 16, 384, 160, 3),
-])
-def test_conv_halo(cfg, B, H, W, Cin, Cout, split, force_cfg):
-    from cassmantle_amd.ops._ext import ext
-    x = rnd(B, H, W, Cin, seed=131)
-    w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=132)
-    b = rnd(Cout, scale=0.1, seed=133)
-    cb = rnd(B, Cout, scale=0.1, seed=134)
-    res = rnd(B, H, W, Cout, seed=135)
-    st = ops.new_stats(B, Cout, DEV)
-    force_cfg(cfg, split)
-    out = ops.conv2d(x, w, b, stride=1, padding=1, residual=res, chan_bias=cb, stats=st)
-    assert tuple(ext().gemm_last_plan()) == (cfg, split)
-    exp = ref.conv2d(x, w, b, 1, 1, res, False, cb)
-    assert out.shape == exp.shape and rel_err(out, exp) < 1e-2
-    exp_st = ops.new_stats(B, Cout, DEV)
-    ops.channel_stats_ref(out, exp_st)
-    assert rel_err(ops.stats_to_float(st), ops.stats_to_float(exp_st)) < 1e-4
-
-
-@pytest.mark.parametrize("cfg", [24, 25])
-def test_conv_halo_ineligible_falls_back(cfg, force_cfg):
-    """shapes the halo kernel does not take (stride 2, Wo % 16, Cin % 64) run another kernel"""
-    from cassmantle_amd.ops._ext import ext
-    for (B, H, W, Cin, Cout, stride) in [(2, 32, 32, 128, 128, 2), (1, 24, 24, 128, 128, 1), (1, 32, 32, 96, 64, 1)]:
-        x = rnd(B, H, W, Cin, seed=136)
-        w = rnd(Cout, 3, 3, Cin, scale=(9 * Cin) ** -0.5, seed=137)
-        force_cfg(cfg)
-        out = ops.conv2d(x, w, None, stride=stride, padding=1)
-        assert tuple(ext().gemm_last_plan())[0] != cfg
-        assert rel_err(out, ref.conv2d(x, w, None, stride, 1, None, False, None)) < 1e-2
-
-
-def test_conv_halo_bitwise_repeatable(force_cfg):
-    """no race between the halo / weight DMA and the fragment reads: 20 runs, one result"""
-    x = rnd(4, 64, 64, 640, seed=138)
-    w = rnd(320, 3, 3, 640, scale=(9 * 640) ** -0.5, seed=139)
-    force_cfg(24)
-    a = ops.conv2d(x, w, None)
-    for _ in range(20):
-        assert torch.equal(ops.conv2d(x, w, None), a)
 
 
 @pytest.mark.parametrize("M,N,K,resid", [(2048, 1280, 1280, True), (512, 1280, 1280, False), (300, 640, 320, True)])

@@ -1,6 +1,6 @@
 """Host-side sanitizer runs of the native GEMM planner / tuning table.
 
-tests/native/planner_sanitize.cpp is linked against ops/csrc/gemm.hip + gemm_areg.hip + gemm_halo.hip (tile
+tests/native/planner_sanitize.cpp is linked against ops/csrc/gemm.hip + gemm_areg.hip (tile
 launchers stubbed) and built twice with hipcc, sanitizers on the HOST side only
 (``-Xarch_host -fsanitize=...``; GPU sanitizers are not available on this pool): ASan + UBSan,
 and TSan.  The driver plans GEMMs from 4 threads while the tuning table is loaded and cleared --
@@ -18,8 +18,7 @@ CSRC = os.path.join(ROOT, "cassmantle_amd", "ops", "csrc")
 DRIVER = os.path.join(ROOT, "tests", "native", "planner_sanitize.cpp")
 OUT = os.path.join(ROOT, "build", "native")
 HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
-SRCS = [os.path.join(CSRC, "gemm.hip"), os.path.join(CSRC, "gemm_areg.hip"), os.path.join(CSRC, "gemm_halo.hip"),
-        DRIVER]
+SRCS = [os.path.join(CSRC, "gemm.hip"), os.path.join(CSRC, "gemm_areg.hip"), DRIVER]
 
 
 def _build(name, flags):

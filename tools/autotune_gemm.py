@@ -26,7 +26,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cassmantle_amd import ops  # noqa: E402
 from cassmantle_amd.ops._ext import ext  # noqa: E402
 
-CFGS = list(range(31))   # 15 = A-in-registers short-K kernel, 16 = 128x80 deep ring, 17-19 register-staged, 20 = pp 128x160, 21 = pp 128x128, 22/23 = pp 128x64 / 256x64, 24/25 = halo-staged 3x3 conv 256x160 / 128x160, 26/27 = 8-wave 128x80 / 128x64 deep ring, 28 = 16-wave 128x64, 29/30 = 8-wave 128x128 / 256x80
+# the live tile configs (gemm.hip is_live_cfg): 0-10 4/8-wave and ping-pong tiles, 12-14 deep ring,
+# 15 = A-in-registers short-K kernel, 16 = 128x80 deep ring, 20-22 = pp 128x160 / 128x128 / 128x64,
+# 26/27 = 8-wave 128x80 / 128x64 deep ring
+CFGS = [*range(0, 11), 12, 13, 14, 15, 16, 20, 21, 22, 26, 27]
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
 
 
