@@ -209,9 +209,16 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __
 }
 
 // GroupNorm apply from producer-accumulated per-channel statistics (GEMM epilogue, p.stats):
-// each block first folds the Cg channel sums of every group of its image into (mean, rstd) in
-// LDS (fp64), then streams rows exactly like gn_apply_kernel.  A channel concatenation
-// (UNet up-block skips) reads channels >= Ca from the second producer's statistics.
+// each block folds the Cg channel sums of every group of its image into (mean, rstd) in LDS
+// (fp64), then streams rows.  A channel concatenation (UNet up-block skips) reads channels >= Ca
+// from the second producer's statistics.
+//
+// Latency structure (round 4): these applies are short (2.6-21 MB) and were bound by three
+// SERIAL memory round trips per block -- statistics fold, then gamma / beta, then the first rows
+// -- not by bandwidth (0.5-5 TB/s, profiles/r3_membound_bandwidth.jsonl).  Now the block's first
+// row group and gamma / beta are issued BEFORE the statistics loads, so the three latencies
+// overlap, and the row loop is software-pipelined (the next row group's loads are issued before
+// the current one is normalised and stored).
 template <int VPT>
 __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ x2,
@@ -228,38 +235,81 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
   const int b = blockIdx.y;
   const int Cg = C / G;
   const int Cb = C - Ca;
-  // fold the Cg channel (sum, sumsq) pairs of every group straight from global memory with TPG
-  // threads per group (all loads of a thread in flight together), exact int64 sums combined
-  // across the TPG lanes by shuffles, then fp64 mean / rstd.  (The previous prologue staged all
-  // C pairs in LDS and folded each group serially in one thread: Cg = 80 dependent LDS reads per
-  // block at C = 2560, which made the 16^2 / 8^2 applies latency-bound.)
+  const int tv = tid % T, rl = tid / T;
+  const bool act = rl < R;                 // row lanes beyond R only help with the fold
+  const long long rbeg = (long long)blockIdx.x * rows_per_block;
+  const long long rend = min(S, rbeg + rows_per_block);
+  uint16_t* yb = y + (long long)b * S * C;
+  // source of each of this thread's 8-channel vectors: the input itself, or for a channel
+  // concatenation [x | x2] (UNet up-block skips, never materialised) x rows of Ca channels and
+  // x2 rows of C - Ca channels (Ca % 8 == 0: a vector never straddles the two)
+  const uint16_t* src[VPT];
+  int lds_[VPT];
+  bool von[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    von[j] = act && (tv + T * j) < V;
+    const int c0 = (von[j] ? tv + T * j : 0) * 8;     // (idle lanes read a valid vector)
+    if (x2 == nullptr) {
+      src[j] = x + (long long)b * S * C + c0;
+      lds_[j] = C;
+    } else if (c0 < Ca) {
+      src[j] = x + (long long)b * S * Ca + c0;
+      lds_[j] = Ca;
+    } else {
+      src[j] = x2 + (long long)b * S * Cb + (c0 - Ca);
+      lds_[j] = Cb;
+    }
+  }
+  // ---- 1. the first row group and gamma / beta in flight before anything else
+  uint4 u[GN_UNROLL][VPT];
+  long long r = rbeg + rl;
+  // unconditional loads at clamped rows (a per-element "load or zero" select makes hipcc branch
+  // around every load and wait for each in turn)
+  auto load_group = [&](long long r0) {
+#pragma unroll
+    for (int k = 0; k < GN_UNROLL; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const long long rr = min(r0 + (long long)k * R, rend - 1);
+        u[k][j] = *reinterpret_cast<const uint4*>(src[j] + rr * lds_[j]);
+      }
+  };
+  load_group(r);
+  uint4 gv[VPT], bv[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int v = von[j] ? tv + T * j : 0;
+    gv[j] = *reinterpret_cast<const uint4*>(gamma + v * 8);
+    bv[j] = *reinterpret_cast<const uint4*>(beta + v * 8);
+  }
+  // ---- 2. fold the Cg channel (sum, sumsq) pairs of every group with TPG threads per group (all
+  // loads of a thread in flight together), exact int64 sums combined across the TPG lanes by
+  // shuffles, then fp64 mean / rstd
   const int tpg = G >= GN_THREADS ? 1 : (GN_THREADS / G >= 8 ? 8 : (GN_THREADS / G >= 4 ? 4 : (GN_THREADS / G >= 2 ? 2 : 1)));
   for (int g0 = 0; g0 < G; g0 += GN_THREADS / tpg) {
     const int g = g0 + tid / tpg, sub = tid % tpg;
     long long si = 0, qi = 0;
     if (g < G) {
-      // up to 16 loads of a thread issued together (unrolled): a rolled loop waited for each
-      // load in turn, ~10 dependent HBM round trips at Cg = 80, and made the 16^2 / 8^2 applies
-      // (5-10 MB) take 9-10 us whatever their size (profiles/r3_membound_bandwidth.jsonl)
       const int c0 = g * Cg + sub, c1 = (g + 1) * Cg;
       longlong2 v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {          // unconditional loads (clamped index) ...
-        const int c = min(c0 + u * tpg, c1 - 1);
-        const long long* src = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
-        v[u] = *reinterpret_cast<const longlong2*>(src);
+      for (int q = 0; q < 16; ++q) {          // unconditional loads (clamped index) ...
+        const int c = min(c0 + q * tpg, c1 - 1);
+        const long long* sp = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
+        v[q] = *reinterpret_cast<const longlong2*>(sp);
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {          // ... then the sums of the live ones
-        const bool live = c0 + u * tpg < c1;
-        si += live ? v[u].x : 0;
-        qi += live ? v[u].y : 0;
+      for (int q = 0; q < 16; ++q) {          // ... then the sums of the live ones
+        const bool live = c0 + q * tpg < c1;
+        si += live ? v[q].x : 0;
+        qi += live ? v[q].y : 0;
       }
       for (int c = c0 + 16 * tpg; c < c1; c += tpg) {
-        const long long* src = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
-        const longlong2 v = *reinterpret_cast<const longlong2*>(src);
-        si += v.x;
-        qi += v.y;
+        const long long* sp = c < Ca ? sa + ((long long)b * Ca + c) * 2 : sb + ((long long)b * Cb + (c - Ca)) * 2;
+        const longlong2 vv = *reinterpret_cast<const longlong2*>(sp);
+        si += vv.x;
+        qi += vv.y;
       }
     }
     for (int o = 1; o < tpg; o <<= 1) {    // tpg lanes of a group are adjacent within one wave
@@ -277,75 +327,46 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
     }
   }
   __syncthreads();
-  const int tv = tid % T, rl = tid / T;
-  if (rl >= R) return;
+  if (!act) return;
   float sc[VPT][8], sf[VPT][8];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int v = tv + T * j;
-    if (v >= V) continue;
     float ga[8], be[8];
-    unpack8(*reinterpret_cast<const uint4*>(gamma + v * 8), ga);
-    unpack8(*reinterpret_cast<const uint4*>(beta + v * 8), be);
+    unpack8(gv[j], ga);
+    unpack8(bv[j], be);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int g = (v * 8 + i) / Cg;
+      const int g = von[j] ? (v * 8 + i) / Cg : 0;
       sc[j][i] = ga[i] * gst[2 * g + 1];
       sf[j][i] = be[i] - gst[2 * g] * sc[j][i];
     }
   }
-  const long long rbeg = (long long)blockIdx.x * rows_per_block;
-  const long long rend = min(S, rbeg + rows_per_block);
-  uint16_t* yb = y + (long long)b * S * C;
-  // source of each of this thread's 8-channel vectors: the input itself, or for a channel
-  // concatenation [x | x2] (UNet up-block skips, never materialised) x rows of Ca channels and
-  // x2 rows of C - Ca channels (Ca % 8 == 0: a vector never straddles the two)
-  const uint16_t* src[VPT];
-  int lds_[VPT];
-#pragma unroll
-  for (int j = 0; j < VPT; ++j) {
-    const int c0 = (tv + T * j) * 8;
-    if (x2 == nullptr) {
-      src[j] = x + (long long)b * S * C + c0;
-      lds_[j] = C;
-    } else if (c0 < Ca) {
-      src[j] = x + (long long)b * S * Ca + c0;
-      lds_[j] = Ca;
-    } else {
-      src[j] = x2 + (long long)b * S * Cb + (c0 - Ca);
-      lds_[j] = Cb;
-    }
-  }
-  auto emit = [&](long long r, int j, uint4 u) {
+  auto emit = [&](long long rr, int j, uint4 w) {
     float f[8];
-    unpack8(u, f);
+    unpack8(w, f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float o = fmaf(f[i], sc[j][i], sf[j][i]);
       f[i] = silu ? silu_f(o) : o;
     }
-    *reinterpret_cast<uint4*>(yb + r * C + (tv + T * j) * 8) = pack8(f);
+    *reinterpret_cast<uint4*>(yb + rr * C + (tv + T * j) * 8) = pack8(f);
   };
-  long long r = rbeg + rl;
-  for (; r + (GN_UNROLL - 1) * R < rend; r += GN_UNROLL * R) {
-    uint4 u[GN_UNROLL][VPT];
+  // ---- 3. software-pipelined row loop: group i + 1 is in flight while group i is stored
+  for (; r < rend; r += GN_UNROLL * R) {
+    uint4 cur[GN_UNROLL][VPT];
 #pragma unroll
     for (int k = 0; k < GN_UNROLL; ++k)
 #pragma unroll
-      for (int j = 0; j < VPT; ++j) {
-        const int v = tv + T * j;
-        if (v < V) u[k][j] = *reinterpret_cast<const uint4*>(src[j] + (r + (long long)k * R) * lds_[j]);
-      }
+      for (int j = 0; j < VPT; ++j) cur[k][j] = u[k][j];
+    const long long rn = r + (long long)GN_UNROLL * R;
+    if (rn < rend) load_group(rn);
 #pragma unroll
     for (int k = 0; k < GN_UNROLL; ++k)
 #pragma unroll
       for (int j = 0; j < VPT; ++j)
-        if (tv + T * j < V) emit(r + (long long)k * R, j, u[k][j]);
+        if (von[j] && r + (long long)k * R < rend) emit(r + (long long)k * R, j, cur[k][j]);
   }
-  for (; r < rend; r += R)
-#pragma unroll
-    for (int j = 0; j < VPT; ++j)
-      if (tv + T * j < V) emit(r, j, *reinterpret_cast<const uint4*>(src[j] + r * lds_[j]));
 }
 
 // per-channel sum / sum-of-squares of an NHWC tensor, atomically added into [B][C][2]

@@ -26,7 +26,7 @@ CONV_SHAPES = [(8, 16, 16, 1280, 1280), (8, 16, 16, 2560, 1280), (8, 8, 8, 1280,
 ITERS = 30
 
 
-def run():
+def run(gn_only: bool = False):
     import torch
     from cassmantle_amd import ops
     from cassmantle_amd.ops._ext import ext
@@ -53,7 +53,7 @@ def run():
         nbytes = 2 * x.numel() * 2
         print(json.dumps({"kernel": "gn_apply_cs", "shape": list(shape), "us": round(us, 2), "bytes": nbytes,
                           "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
-    for B, H, W, Cin, Cout in CONV_SHAPES:
+    for B, H, W, Cin, Cout in ([] if gn_only else CONV_SHAPES):
         x = (torch.randn(B, H, W, Cin, device="cuda") * 0.5).to(torch.bfloat16)
         w = (torch.randn(Cout, 3, 3, Cin, device="cuda") * (9 * Cin) ** -0.5).to(torch.bfloat16)
         st = ops.new_stats(B, Cout, "cuda")
@@ -93,8 +93,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", default=None, help="rocprofv3 kernel trace of a previous run")
     ap.add_argument("--lines", default=None, help="that run's JSON output (for --trace)")
+    ap.add_argument("--gn-only", action="store_true", help="only the GroupNorm applies")
     a = ap.parse_args()
     if a.trace:
         from_trace(a.trace, [json.loads(x) for x in open(a.lines) if x.startswith("{")])
     else:
-        run()
+        run(a.gn_only)
