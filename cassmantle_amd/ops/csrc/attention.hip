@@ -27,6 +27,16 @@ namespace {
 
 constexpr int KT = 64;  // keys per tile
 
+// v_permlane32_swap of a value with itself: one of the two results is this lane's own value and
+// the other lane l ^ 32's (lanes 0-31 get it in .y, lanes 32-63 in .x), so a cross-half max or
+// sum is fmax(.x, .y) / .x + .y in every lane -- a VALU op instead of __shfl_xor's ds_bpermute
+// round trip through the LDS unit (guide T12)
+CM_DEVICE float2 both_halves(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 template <int DQK, int DO>
 struct AttnGeom {
   static constexpr int KCH = DQK / 8;                         // 16B chunks per K row
@@ -146,20 +156,25 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     v_lds[i] = key < KT ? key * G::VSTR + ch * 8 : -1;
     v_src[i] = Vp + (long long)key * a.v_sn + ch * 8;
   }
+  // branch-free staging loads: every lane loads (an out-of-range or padding chunk reads the
+  // K / V base row instead) and the padding value is selected afterwards -- a conditional load
+  // made hipcc wrap every load in an exec-mask branch (s_and_saveexec / s_cbranch_execz)
   auto gload = [&](int t) {
     const int kbase = t * KT;
     const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
 #pragma unroll
     for (int i = 0; i < KLD; ++i) {
-      uint4 v = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
-      if (k_use[i] && kbase + k_key[i] < nk) v = *reinterpret_cast<const uint4*>(k_src[i] + ko);
-      kr[i] = v;
+      const bool ok = k_use[i] && kbase + k_key[i] < nk;
+      const uint4 v = *reinterpret_cast<const uint4*>(ok ? k_src[i] + ko : Kp);
+      const uint4 z = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+      kr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
     }
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
-      uint4 v = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
-      if (v_use[i] && kbase + v_key[i] < nk) v = *reinterpret_cast<const uint4*>(v_src[i] + vo);
-      vr[i] = v;
+      const bool ok = v_use[i] && kbase + v_key[i] < nk;
+      const uint4 v = *reinterpret_cast<const uint4*>(ok ? v_src[i] + vo : Vp);
+      const uint4 z = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+      vr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
     }
   };
   auto lstore = [&](int bo) {   // bo: element offset of the target buffer
@@ -176,6 +191,11 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     lstore(0);
   }
   __syncthreads();
+  // static priority for the second-dispatched half of an 8-wave block (MI355X_MICROARCH.md
+  // "Two waves per SIMD" item 4): it otherwise loses every VALU arbitration to its older partner
+  if constexpr (NW == 8) {
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
 
   // tr-read lane geometry (T10): group g = lane>>4, i = lane&15 -> row q' = i>>2, col 4*(i&3)
   const int tg = lane >> 4, ti = lane & 15;
@@ -227,7 +247,10 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    {
+      const float2 hm = both_halves(mx);
+      mx = fmaxf(hm.x, hm.y);
+    }
     if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
       // a real branch: without the volatile asm hipcc if-converts this block and rescales O
       // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
@@ -270,7 +293,8 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
           sacc[hf][r] = pv;
           rs += pv;
         }
-      rs += __shfl_xor(rs, 32, 64);
+      const float2 hs = both_halves(rs);
+      rs = hs.x + hs.y;
     }
     l_run += rs;
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# full check of the tree (tests, smoke, bench, profiles) + the GroupNorm apply A/B
+# full check of the tree (tests, smoke, bench) + the GroupNorm apply and attention A/Bs
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-SKIP_PROF=${SKIP_PROF:-0} bash tools/gpu/full_check.sh ${1:-r4b} || exit 1
-bash tools/gpu/gn_ab.sh
+SKIP_PROF=1 bash tools/gpu/full_check.sh ${1:-r4b} || exit 1
+bash tools/gpu/gn_ab.sh || exit 1
+bash tools/gpu/attn_ab.sh
