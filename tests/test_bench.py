@@ -50,3 +50,19 @@ def test_bench_failing_rank_fails_the_job():
     r = _run(["--gpus", "2", "--model", "nope", "--steps", "1", "--warmup", "0", "--no-score"], timeout=120)
     assert r.returncode != 0
     assert not _json_lines(r.stdout)
+
+
+def test_bench_live_supervised_topology():
+    """tools/bench_live.py --gpus 2: front-end + 2 supervised workers (gloo on the CPU), both
+    rooms drawn every round while the front-end scores"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_live.py"), "--gpus", "2", "--model", "tiny",
+                        "--players", "4", "--seconds", "3", "--idle-s", "1"], capture_output=True, text=True,
+                       timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json_lines(r.stdout)[-1]
+    assert out["topology"] == "supervised" and out["n_gpus"] == 2
+    assert out["devices"] == ["cpu:0", "cpu:1"] and not out["retired"]
+    assert out["rounds"] >= 1 and out["images_per_s"] > 0 and out["requests"] > 0

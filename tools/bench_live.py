@@ -19,7 +19,15 @@ Rank 0 prints one JSON line: whole-job images/s during the overlapped phase, p50
 latency idle vs under load (max over ranks), and requests served.
 
     python tools/bench_live.py --seconds 30
-    torchrun --nproc-per-node 8 tools/bench_live.py --players 64
+    python tools/bench_live.py --gpus 8 --players 64          # the supervised topology serve.py uses
+    torchrun --nproc-per-node 8 tools/bench_live.py --players 64   # the legacy torchrun layout
+
+``--gpus N`` (no torchrun environment) runs the topology ``serve.py --gpus N`` really uses: this
+process is the front-end; it spawns one supervised worker process per GPU BEFORE it touches a
+GPU (``parallel.supervisor.GroupSupervisor``), then scores on GPU 0 beside worker 0.  Every
+generation round gives each of the N rooms (one per GPU) its ``--batch`` images: C1 job list to
+the workers, local generation, C2 device-resident gather to the group leader, one pipe hop of
+uint8 images to the front-end.  ``--model tiny`` runs the same topology on the CPU (gloo).
 """
 import argparse
 import asyncio
@@ -60,6 +68,8 @@ def parse():
                     help="as serve.py's GameConfig.score_topology: rank-0 scoring, or micro-batches of "
                          ">= --shard-min pairs split over every rank (C1 broadcast + C3 gather, parallel/scoring.py)")
     ap.add_argument("--shard-min", type=int, default=256)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="supervised topology on this many devices (front-end + one worker process each)")
     return ap.parse_args()
 
 
@@ -84,8 +94,94 @@ async def run_players(scorer, n, seconds, think_ms, seed):
     return lat
 
 
+def main_supervised(a) -> None:
+    """The serving topology of ``serve.py --gpus N``: front-end (scoring, game state) plus a
+    supervised worker group (generation), see the module docstring."""
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    from cassmantle_amd.pipeline import SPECS
+    from cassmantle_amd.scoring.batcher import BatchingScorer
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+
+    gpu = torch.cuda.device_count() > 0          # (does not initialise the GPU on this image)
+    n = a.gpus
+    devices = [f"cuda:{i}" for i in range(n)] if gpu else [f"cpu:{i}" for i in range(n)]
+    spec = SPECS[a.model]
+    cfg = Config()
+    cfg.model.image_model = a.model
+    cfg.model.resolution = spec.resolution
+    cfg.model.steps = spec.steps
+    cfg.model.scheduler = spec.scheduler
+    cfg.model.guidance_scale = spec.guidance
+    cfg.model.device = "cuda" if gpu else "cpu"
+    rooms = [""] + [str(i) for i in range(1, n)]
+    t_start = time.perf_counter()
+    sup = GroupSupervisor(cfg, devices, rooms, window_s=0.05, start_timeout_s=1200)
+    if not sup.wait_ready(1500) or not sup.live_devices():
+        raise SystemExit(f"worker group did not start: {sup.status()}")
+    print(f"[live] worker group up on {sup.live_devices()} in {time.perf_counter() - t_start:.1f} s",
+          file=sys.stderr, flush=True)
+    dev = torch.device("cuda:0" if gpu else "cpu")
+    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
+    scorer = BatchingScorer(backend, 0.01, window_ms=a.window_ms)
+    gen = SyntheticPromptGenerator(salt=0)
+    seeds_txt, styles = load_seeds(), load_styles()
+
+    def prompts(step, r):
+        return [image_prompt(styles[(step + j) % len(styles)],
+                             gen.generate(seeds_txt[(r + step + j) % len(seeds_txt)] + "\n", True),
+                             "A {style} style piece depicting the following: ") for j in range(a.batch)]
+
+    def one_round(step) -> int:
+        futs = [sup.submit(room, prompts(step, i), [i * 10000 + step * 10 + j for j in range(a.batch)])
+                for i, room in enumerate(rooms)]
+        return sum(len(f.result(timeout=1800)) for f in futs)
+
+    one_round(0)                                   # warm: graph capture on every worker
+    print("[live] warm round done", file=sys.stderr, flush=True)
+    asyncio.run(run_players(scorer, min(a.players, 4), 1.0, a.think_ms, 99))
+    idle = asyncio.run(run_players(scorer, a.players, a.idle_s, a.think_ms, 0))
+    print(f"[live] idle phase done: {len(idle)} requests", file=sys.stderr, flush=True)
+    done = {"images": 0, "rounds": 0}
+    stop = threading.Event()
+
+    def gen_loop():
+        step = 1
+        while not stop.is_set():
+            done["images"] += one_round(step)
+            done["rounds"] += 1
+            step += 1
+            print(f"[live] {done['images']} images", file=sys.stderr, flush=True)
+
+    th = threading.Thread(target=gen_loop, daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    load = asyncio.run(run_players(scorer, a.players, a.seconds, a.think_ms, 7))
+    imgs_at_stop = done["images"]
+    elapsed = time.perf_counter() - t0
+    stop.set()
+    th.join()
+    st = sup.status()
+    sup.close()
+
+    def pct(x, q):
+        return float(np.percentile(np.asarray(x), q)) if x else float("nan")
+    print(json.dumps({
+        "metric": "live round: images/s with overlapped streaming guess scoring (BASELINE config 5)",
+        "topology": "supervised", "images_per_s": round(imgs_at_stop / elapsed, 3), "n_gpus": n,
+        "devices": st["live_devices"], "players": a.players, "think_ms": a.think_ms,
+        "idle_p50_ms": round(pct(idle, 50), 3), "idle_p99_ms": round(pct(idle, 99), 3),
+        "load_p50_ms": round(pct(load, 50), 3), "load_p99_ms": round(pct(load, 99), 3), "requests": len(load),
+        "rounds": done["rounds"], "gather_us_p50": st["gather_us_p50"], "retired": st["retired"],
+        "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
+        "config": {"model": a.model, "batch_per_room": a.batch, "rooms": len(rooms)}}), flush=True)
+
+
 def main():
     a = parse()
+    if a.gpus is not None and "WORLD_SIZE" not in os.environ:
+        return main_supervised(a)
     from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
     from cassmantle_amd.parallel import dist as cdist
     from cassmantle_amd.pipeline import SPECS, StableDiffusion
