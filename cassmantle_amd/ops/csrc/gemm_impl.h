@@ -71,14 +71,16 @@ CM_DEVICE void add4(float* o, uint2 v) {
 // mean_m * wsum[n..n+3]) for the W rows n..n+3
 CM_DEVICE float2 ln_row(const GemmArgs& p, int m) {
   if (p.ln_rows_fx != nullptr) {
-    // fp32 decode (the fp64 form pushed the 256x256 ping-pong tiles into scratch): the fixed-
-    // point sums are exact; mean = s / K, var = q / K - mean^2 in fp32 (LayerNorm inputs here
-    // are residual streams with |mean| ~ std, far from the cancellation range)
+    // the fixed-point sums are exact; mean and var = q / K - mean^2 are formed in fp64, so rows
+    // with |mean| >> std keep their variance (fp32 lost ~log2(mean^2 / var) bits of it to the
+    // cancellation).  This runs once per ROW of the LDS-staged epilogue (the per-4-
+    // column form of round 3 pushed the 256x256 ping-pong tiles into scratch;
+    // tests/test_kernel_registers.py guards it)
     const longlong2 v = reinterpret_cast<const longlong2*>(p.ln_rows_fx)[m];
-    const float inv = 1.f / (float)p.K;
-    const float mean = (float)v.x * (inv * (float)(1.0 / STAT_SCALE_SUM));
-    const float var = fmaxf((float)v.y * (inv * (float)(1.0 / STAT_SCALE_SQ)) - mean * mean, 0.f);
-    return make_float2(mean, rsqrtf(var + p.ln_eps));
+    const double inv = 1.0 / (double)p.K;
+    const double mean = (double)v.x * (inv * (1.0 / STAT_SCALE_SUM));
+    const double var = fmax((double)v.y * (inv * (1.0 / STAT_SCALE_SQ)) - mean * mean, 0.0);
+    return make_float2((float)mean, rsqrtf((float)var + p.ln_eps));
   }
   return reinterpret_cast<const float2*>(p.ln_rows)[m];
 }

@@ -923,6 +923,31 @@ def test_gemm_row_stats_feed_folded_layernorm(M, N, K, resid):
     assert rel_err(out, out_pass) < 5e-3      # (bf16 rounding of two different kernels)
 
 
+@pytest.mark.parametrize("offset", [8.0, 24.0])
+def test_row_stats_layernorm_with_large_row_means(offset):
+    """the folded LayerNorm derives var = E[x^2] - mean^2 from the producer's fixed-point
+    row sums; rows whose |mean| is many times their std (a residual stream plus a large constant)
+    must still normalise like the statistics-pass path and the fp32 reference (the variance is now
+    formed in fp64).  bf16 itself only resolves std ~ |mean| / 256, so offsets stay <= 24 std."""
+    M, N, K = 1024, 1280, 1280
+    x = rnd(M, K, seed=161)
+    w = rnd(N, K, scale=K ** -0.5, seed=162)
+    r = rnd(M, N, seed=163) + offset                      # residual stream with a large row mean
+    rs = ops.new_stats(1, M, DEV).view(M, 2)
+    y = ops.linear(x, w, None, residual=r, row_stats=rs)
+    yf = y.float()
+    assert (yf.mean(1).abs() / yf.std(1)).min().item() > 0.5 * offset / 1.5
+    g = rnd(N, seed=164) * 0.5 + 1
+    be = rnd(N, seed=165) * 0.1
+    w2 = rnd(640, N, scale=N ** -0.5, seed=166)
+    fold = ops.ln_fold(g, be, w2)
+    out = ops.ln_linear(y, g, be, 1e-5, w2, fold=fold, row_stats=rs)
+    out_pass = ops.ln_linear(y, g, be, 1e-5, w2, fold=fold)
+    exp = ref.linear(ref.layer_norm(y, g, be, 1e-5), w2)
+    assert rel_err(out, exp) < 2e-2, rel_err(out, exp)
+    assert rel_err(out, out_pass) < 1e-2, rel_err(out, out_pass)
+
+
 @pytest.mark.parametrize("B,S,C,N", [(2, 4096, 320, 320), (2, 1024, 640, 640), (1, 256, 320, 192)])
 def test_gn_linear_folds_groupnorm_into_areg(B, S, C, N):
     """GroupNorm (producer statistics, no SiLU) applied to the A rows inside the A-in-registers
