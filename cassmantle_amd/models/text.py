@@ -155,13 +155,13 @@ class CLIPTextEncoder(nn.Module):
             eos_rows = (torch.arange(B) * L + (ids == self.tokenizer.eos).int().argmax(dim=1)).int()
         if not graphs or torch.device(device).type != "cuda" or ops.get_mode() != "hip":
             # int32 ids, converted on the host: the embedding gather takes them as they are
-            return self.forward(ids.int().to(device), output_hidden,
-                                None if eos_rows is None else eos_rows.to(device))
+            return self.forward(ops.h2d(ids.int(), device), output_hidden,
+                                None if eos_rows is None else ops.h2d(eos_rows, device))
         key = (tuple(ids.shape), output_hidden, str(device))
         g = self.__dict__.setdefault("_graphs", {}).get(key)
         if g is None:
-            sid = ids.int().to(device)
-            seos = None if eos_rows is None else eos_rows.to(device)
+            sid = ops.h2d(ids.int(), device)
+            seos = None if eos_rows is None else ops.h2d(eos_rows, device)
             s = torch.cuda.Stream(device=device)
             s.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(s):
@@ -173,9 +173,9 @@ class CLIPTextEncoder(nn.Module):
                 out = self.forward(sid, output_hidden, seos)
             g = self._graphs[key] = (graph, sid, seos, out)
         graph, sid, seos, (hidden, pooled) = g
-        sid.copy_(ids.int())
+        sid.copy_(ids.int().pin_memory(), non_blocking=True)
         if seos is not None:
-            seos.copy_(eos_rows)
+            seos.copy_(eos_rows.pin_memory(), non_blocking=True)
         graph.replay()
         h = ops.copy_(torch.empty_like(hidden), hidden)
         p = None if pooled is None else ops.copy_(torch.empty_like(pooled), pooled)

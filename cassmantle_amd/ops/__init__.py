@@ -106,6 +106,17 @@ _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "
 STAT_SCALE = (2.0 ** 24, 2.0 ** 16)
 
 
+def h2d(t: torch.Tensor, device) -> torch.Tensor:
+    """Host tensor -> ``device`` without blocking the host: through pinned memory with a
+    non-blocking copy on the current stream.  A plain ``.to(device)`` of pageable memory
+    synchronises the stream (PyTorch's blocking copy), so a generation's input upload used to
+    wait for every kernel the previous generation had queued on the pipeline stream."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def new_stats(B: int, C: int, device) -> torch.Tensor:
     """A zeroed statistics buffer for ``stats=`` arguments: int64 [B, C, 2]."""
     return zero_(torch.empty((B, C, 2), device=device, dtype=torch.int64))

@@ -195,7 +195,7 @@ class StableDiffusion:
                 pooled = p
         ctx = ops.concat_last(hs[0], hs[1]) if len(hs) == 2 else torch.cat(hs, dim=-1)
         R = self.spec.resolution
-        tid = torch.tensor([R, R, 0, 0, R, R], dtype=torch.float32).repeat(len(texts), 1).to(self.device)
+        tid = ops.h2d(torch.tensor([R, R, 0, 0, R, R], dtype=torch.float32).repeat(len(texts), 1), self.device)
         return ctx, {"time_ids": tid, "text_embeds": pooled}
 
     # ------------------------------------------------------------------ denoise
@@ -295,7 +295,7 @@ class StableDiffusion:
         for s in seeds:
             g = torch.Generator().manual_seed(int(s))
             xs.append(torch.randn((h, h, 4), generator=g, dtype=torch.float32))
-        return (torch.stack(xs) * plan.init_sigma).to(self.device)
+        return ops.h2d(torch.stack(xs) * plan.init_sigma, self.device)
 
     @torch.no_grad()
     def generate_tensor(self, prompts: Sequence[str], negative: str, seeds: Sequence[int],
