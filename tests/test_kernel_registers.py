@@ -34,6 +34,6 @@ def _scratch(tu):
 
 
 @pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
-@pytest.mark.parametrize("tu", ["gemm_pp_c2", "gemm_pp_c0", "gemm_c0_buf", "gemm_areg"])
+@pytest.mark.parametrize("tu", ["gemm_pp_c2", "gemm_pp_c0", "gemm_c0_buf", "gemm_areg", "attention", "norm"])
 def test_default_kernels_do_not_spill(tu):
     assert _scratch(tu) == []
