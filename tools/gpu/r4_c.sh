@@ -1,0 +1,9 @@
+#!/bin/bash
+# per-eval kernel profiles + PMC tables of SD-1.5 and SDXL (fp8 attention) on one box
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+tag=${1:-r4c}
+bash tools/gpu/profile.sh ${tag}_sd15 sd15 10 24 || exit 1
+bash tools/gpu/profile.sh ${tag}_sdxl sdxl 4 10 --batch 1 --fp8-attention || exit 1
+TOP=14 bash tools/gpu/pmc_table.sh ${tag}_sd15 --model sd15 --denoise-steps 2 || exit 1
+TOP=14 bash tools/gpu/pmc_table.sh ${tag}_sdxl --model sdxl --batch 1 --fp8-attention --denoise-steps 2 || exit 1
