@@ -34,9 +34,10 @@ def test_rank_worker_nccl_world1_device_path_matches_generate():
             im = res[(j.room, i)]
             assert im.dtype == np.uint8 and im.shape == (16, 16, 3)
             assert np.array_equal(im, ref[i]), i
-        # a second round reuses the comm stream and the graph-captured step
+        # a second round (batch 1: its own captured step) reuses the comm stream
         res2 = w.run_round(jobs[:1], round_id=8)
-        assert done == [7, 8] and np.array_equal(res2[("", 0)], ref[0])
+        ref1 = gen.generate([jobs[0].prompt], w.negative, [jobs[0].seed])
+        assert done == [7, 8] and np.array_equal(res2[("", 0)], ref1[0])
     finally:
         dist.destroy_process_group()
 
