@@ -27,6 +27,17 @@ namespace {
 
 constexpr int KT = 64;  // keys per tile
 
+// A/B switches of the round-4 micro-changes (tools/gpu/attn_ab.sh; each measured alone)
+#ifndef ATTN_PERMLANE
+#define ATTN_PERMLANE 0
+#endif
+#ifndef ATTN_BRANCHLESS
+#define ATTN_BRANCHLESS 0
+#endif
+#ifndef ATTN_PRIO
+#define ATTN_PRIO 0
+#endif
+
 // v_permlane32_swap of a value with itself: one of the two results is this lane's own value and
 // the other lane l ^ 32's (lanes 0-31 get it in .y, lanes 32-63 in .x), so a cross-half max or
 // sum is fmax(.x, .y) / .x + .y in every lane -- a VALU op instead of __shfl_xor's ds_bpermute
@@ -164,17 +175,29 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
 #pragma unroll
     for (int i = 0; i < KLD; ++i) {
-      const bool ok = k_use[i] && kbase + k_key[i] < nk;
-      const uint4 v = *reinterpret_cast<const uint4*>(ok ? k_src[i] + ko : Kp);
-      const uint4 z = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
-      kr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
+      if constexpr (ATTN_BRANCHLESS) {
+        const bool ok = k_use[i] && kbase + k_key[i] < nk;
+        const uint4 v = *reinterpret_cast<const uint4*>(ok ? k_src[i] + ko : Kp);
+        const uint4 z = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+        kr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
+      } else {
+        uint4 v = make_uint4(k_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+        if (k_use[i] && kbase + k_key[i] < nk) v = *reinterpret_cast<const uint4*>(k_src[i] + ko);
+        kr[i] = v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
-      const bool ok = v_use[i] && kbase + v_key[i] < nk;
-      const uint4 v = *reinterpret_cast<const uint4*>(ok ? v_src[i] + vo : Vp);
-      const uint4 z = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
-      vr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
+      if constexpr (ATTN_BRANCHLESS) {
+        const bool ok = v_use[i] && kbase + v_key[i] < nk;
+        const uint4 v = *reinterpret_cast<const uint4*>(ok ? v_src[i] + vo : Vp);
+        const uint4 z = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+        vr[i] = make_uint4(ok ? v.x : z.x, ok ? v.y : z.y, ok ? v.z : z.z, ok ? v.w : z.w);
+      } else {
+        uint4 v = make_uint4(v_one[i] ? 0x3F80u : 0u, 0, 0, 0);
+        if (v_use[i] && kbase + v_key[i] < nk) v = *reinterpret_cast<const uint4*>(v_src[i] + vo);
+        vr[i] = v;
+      }
     }
   };
   auto lstore = [&](int bo) {   // bo: element offset of the target buffer
@@ -193,7 +216,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   __syncthreads();
   // static priority for the second-dispatched half of an 8-wave block (MI355X_MICROARCH.md
   // "Two waves per SIMD" item 4): it otherwise loses every VALU arbitration to its older partner
-  if constexpr (NW == 8) {
+  if constexpr (NW == 8 && ATTN_PRIO) {
     if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   }
 
@@ -247,9 +270,11 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
-    {
+    if constexpr (ATTN_PERMLANE) {
       const float2 hm = both_halves(mx);
       mx = fmaxf(hm.x, hm.y);
+    } else {
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     }
     if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
       // a real branch: without the volatile asm hipcc if-converts this block and rescales O
@@ -293,8 +318,12 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
           sacc[hf][r] = pv;
           rs += pv;
         }
-      const float2 hs = both_halves(rs);
-      rs = hs.x + hs.y;
+      if constexpr (ATTN_PERMLANE) {
+        const float2 hs = both_halves(rs);
+        rs = hs.x + hs.y;
+      } else {
+        rs += __shfl_xor(rs, 32, 64);
+      }
     }
     l_run += rs;
 

@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const uint16_t* __
 // row group and gamma / beta are issued BEFORE the statistics loads, so the three latencies
 // overlap, and the row loop is software-pipelined (the next row group's loads are issued before
 // the current one is normalised and stored).
-template <int VPT>
+template <int VPT, int U>
 __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ x2,
                                                                  const long long* __restrict__ sa, int Ca,
@@ -262,13 +262,13 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
     }
   }
   // ---- 1. the first row group and gamma / beta in flight before anything else
-  uint4 u[GN_UNROLL][VPT];
+  uint4 u[U][VPT];
   long long r = rbeg + rl;
   // unconditional loads at clamped rows (a per-element "load or zero" select makes hipcc branch
   // around every load and wait for each in turn)
   auto load_group = [&](long long r0) {
 #pragma unroll
-    for (int k = 0; k < GN_UNROLL; ++k)
+    for (int k = 0; k < U; ++k)
 #pragma unroll
       for (int j = 0; j < VPT; ++j) {
         const long long rr = min(r0 + (long long)k * R, rend - 1);
@@ -353,16 +353,16 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
     *reinterpret_cast<uint4*>(yb + rr * C + (tv + T * j) * 8) = pack8(f);
   };
   // ---- 3. software-pipelined row loop: group i + 1 is in flight while group i is stored
-  for (; r < rend; r += GN_UNROLL * R) {
-    uint4 cur[GN_UNROLL][VPT];
+  for (; r < rend; r += U * R) {
+    uint4 cur[U][VPT];
 #pragma unroll
-    for (int k = 0; k < GN_UNROLL; ++k)
+    for (int k = 0; k < U; ++k)
 #pragma unroll
       for (int j = 0; j < VPT; ++j) cur[k][j] = u[k][j];
-    const long long rn = r + (long long)GN_UNROLL * R;
+    const long long rn = r + (long long)U * R;
     if (rn < rend) load_group(rn);
 #pragma unroll
-    for (int k = 0; k < GN_UNROLL; ++k)
+    for (int k = 0; k < U; ++k)
 #pragma unroll
       for (int j = 0; j < VPT; ++j)
         if (von[j] && r + (long long)k * R < rend) emit(r + (long long)k * R, j, cur[k][j]);
@@ -550,27 +550,44 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        C, G, g.T, g.R, rpb, silu);
 }
 
-void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long* stats_a, int Ca, const long long* stats_b,
-                          const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
-                          int G, float eps, int silu, hipStream_t s) {
-  const GnGeom g = gn_geom(C);
-  // every thread runs whole GN_UNROLL-row iterations (GN_UNROLL independent 16-byte loads in
-  // flight): the old fallback to 2 rows per thread for short grids left one dependent load per
-  // thread at a time and ran the SD-1.5 level-1 apply at ~3.2 TB/s
-  // ... and blocks long enough to amortise the prologue (every block first reads all C channel
-  // statistics, 16 B each: at C = 1280 a 4-row block reads twice its own data): at least 32 rows
-  // and 32 KiB of activations per block, shortened only while that leaves fewer than ~1024 blocks
-  // (the 16^2 / 8^2 levels), and down to half an iteration when even one iteration per thread
-  // leaves fewer than 256 blocks (8^2 x 2560: 2 rows per thread on 256 blocks beats 4 on 128).
-  // profiles/r2_gn_rows_ab.txt has the per-shape A/B; CASSMANTLE_GN_ROWS=-1 restores the
-  // round-1 rule (A/B knob)
-  static const int mode = [] { const char* e = getenv("CASSMANTLE_GN_ROWS"); return e ? atoi(e) : 0; }();
-  const long long step = (long long)GN_UNROLL * g.R;
-  long long rpb, nb;
-  if (mode < 0) {
-    rpb = 8LL * g.R;
-    nb = (S + rpb - 1) / rpb;
-    if (nb * B < 1024) rpb = 2LL * g.R;
+// Apply geometry: 8-channel vectors per thread (VPT in {1, 2, 4}) chosen for the most active
+// threads of the 256 (V = 160 at C = 1280 left 96 idle at VPT 1), U rows per thread in flight,
+// and enough blocks to keep ~GN_APPLY_BLOCKS in flight over the chip (memory-level parallelism:
+// the round-3 rule of >= 32 rows per block left ~2 blocks per CU at the 64^2 level, 2.6 TB/s).
+#ifndef GN_APPLY_GEOM
+#define GN_APPLY_GEOM 1
+#endif
+#ifndef GN_APPLY_U
+#define GN_APPLY_U 8
+#endif
+#ifndef GN_APPLY_BLOCKS
+#define GN_APPLY_BLOCKS 1024
+#endif
+static GnGeom gn_apply_geom(int C) {
+  GnGeom g = gn_geom(C);
+  if (!GN_APPLY_GEOM) return g;
+  int best = -1;
+  for (int vpt = 1; vpt <= 4; vpt *= 2) {
+    const int T = (g.V + vpt - 1) / vpt;
+    if (T > GN_THREADS) continue;
+    const int R = GN_THREADS / T;
+    const int active = R * T;
+    if (active * 10 > best * 11) { best = active; g.VPT = vpt; g.T = T; g.R = R; }   // > 10 % more
+
+  }
+  return g;
+}
+
+template <int VPT, int U>
+static void launch_apply(const uint16_t* x, const uint16_t* x2, const long long* stats_a, int Ca, const long long* stats_b,
+                         const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C, int G,
+                         float eps, int silu, const GnGeom& g, hipStream_t s) {
+  const long long step = (long long)U * g.R;                       // rows per block iteration
+  long long rpb;
+  if (GN_APPLY_GEOM) {
+    const long long per_img = (GN_APPLY_BLOCKS + B - 1) / B;
+    const long long want = (S + per_img - 1) / per_img;
+    rpb = step * ((want + step - 1) / step);
   } else {
     long long want = 32;
     if (want < (32LL << 10) / (2LL * C)) want = (32LL << 10) / (2LL * C);
@@ -578,15 +595,23 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long
     while (rpb > step && ((S + rpb - 1) / rpb) * B < 1024) rpb -= step;
     if (rpb == step && ((S + rpb - 1) / rpb) * B < 256) rpb = step / 2 >= g.R ? step / 2 : g.R;
   }
-  nb = (S + rpb - 1) / rpb;
+  const long long nb = (S + rpb - 1) / rpb;
   const size_t shs = sizeof(float) * 2 * G;
+  hipLaunchKernelGGL((gn_apply_cs_kernel<VPT, U>), dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
+                     stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
+}
+
+void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long* stats_a, int Ca, const long long* stats_b,
+                          const uint16_t* gamma, const uint16_t* beta, uint16_t* y, int B, long long S, int C,
+                          int G, float eps, int silu, hipStream_t s) {
+  const GnGeom g = gn_apply_geom(C);
   if (stats_b == nullptr) Ca = C;
-  if (g.VPT == 1)
-    hipLaunchKernelGGL(gn_apply_cs_kernel<1>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
-                       stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
-  else
-    hipLaunchKernelGGL(gn_apply_cs_kernel<2>, dim3((unsigned)nb, B), dim3(GN_THREADS), shs, s, x, x2, stats_a, Ca,
-                       stats_b, gamma, beta, y, S, C, G, g.T, g.R, rpb, eps, silu);
+  // U rows per thread, at most 16 vector loads (VPT x U) in flight per thread
+  constexpr int U = GN_APPLY_U;
+  constexpr int U2 = U * 2 > 16 ? 8 : U, U4 = U * 4 > 16 ? 4 : U;
+  if (g.VPT == 1) launch_apply<1, U>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
+  else if (g.VPT == 2) launch_apply<2, U2>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
+  else launch_apply<4, U4>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
 }
 
 void launch_channel_stats(const uint16_t* x, long long* stats, int B, long long S, int C, hipStream_t s) {
