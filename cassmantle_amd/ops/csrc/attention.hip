@@ -27,15 +27,18 @@ namespace {
 
 constexpr int KT = 64;  // keys per tile
 
-// A/B switches of the round-4 micro-changes (tools/gpu/attn_ab.sh; each measured alone)
+// A/B switches of the round-4 micro-changes, each measured alone on one box
+// (profiles/r4_attn_switches_ab.txt): the permlane cross-half max/sum and the static priority
+// of the younger half are 1-4 % faster and on; branch-free staging loads (value selects) were
+// 4-12 % SLOWER (their selects are VALU, the contended pipe of this kernel) and are off
 #ifndef ATTN_PERMLANE
-#define ATTN_PERMLANE 0
+#define ATTN_PERMLANE 1
 #endif
 #ifndef ATTN_BRANCHLESS
 #define ATTN_BRANCHLESS 0
 #endif
 #ifndef ATTN_PRIO
-#define ATTN_PRIO 0
+#define ATTN_PRIO 1
 #endif
 
 // v_permlane32_swap of a value with itself: one of the two results is this lane's own value and

@@ -550,15 +550,17 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
                        C, G, g.T, g.R, rpb, silu);
 }
 
-// Apply geometry: 8-channel vectors per thread (VPT in {1, 2, 4}) chosen for the most active
-// threads of the 256 (V = 160 at C = 1280 left 96 idle at VPT 1), U rows per thread in flight,
-// and enough blocks to keep ~GN_APPLY_BLOCKS in flight over the chip (memory-level parallelism:
-// the round-3 rule of >= 32 rows per block left ~2 blocks per CU at the 64^2 level, 2.6 TB/s).
+// Apply geometry: 8-channel vectors per thread (VPT in {1, 2}) chosen for the most active threads
+// of the 256 (V = 160 at C = 1280 left 96 idle at VPT 1), U rows per thread in flight, and
+// ~GN_APPLY_BLOCKS blocks over the chip (the round-3 rule of >= 32 rows per block left ~2 blocks
+// per CU at the 64^2 level).  Same-box A/B of the variants (profiles/r4_gn_apply_variants.txt):
+// 64^2 x 320 16.8 -> 13.0 us, 32^2 x 1280 15.5 -> 14.7, the 16^2 / 8^2 applies unchanged; 8 rows
+// per thread or 2048 blocks were slower on the small levels.
 #ifndef GN_APPLY_GEOM
 #define GN_APPLY_GEOM 1
 #endif
 #ifndef GN_APPLY_U
-#define GN_APPLY_U 8
+#define GN_APPLY_U 4
 #endif
 #ifndef GN_APPLY_BLOCKS
 #define GN_APPLY_BLOCKS 1024
@@ -567,7 +569,7 @@ static GnGeom gn_apply_geom(int C) {
   GnGeom g = gn_geom(C);
   if (!GN_APPLY_GEOM) return g;
   int best = -1;
-  for (int vpt = 1; vpt <= 4; vpt *= 2) {
+  for (int vpt = 1; vpt <= 2; vpt *= 2) {      // (VPT 4 measured 1.1-1.6x slower at C = 2560)
     const int T = (g.V + vpt - 1) / vpt;
     if (T > GN_THREADS) continue;
     const int R = GN_THREADS / T;
