@@ -36,6 +36,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#ifndef GEMM_DIAG_APRO
+#define GEMM_DIAG_APRO 0
+#endif
+
 namespace {
 
 __device__ uint4 g_zero_page[4];   // zero-initialised (per translation unit); padded / out-of-range chunks
@@ -715,6 +719,19 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       for (int i = 0; i < TI; ++i) wf[i] = as_bf16x8(Bs[w_rd[ks] + 16 * 8 * i]);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) af[j] = as_bf16x8(Bs[a_rd[ks] + 16 * 8 * j]);
+#if GEMM_DIAG_APRO
+      // cost probe of a GroupNorm+SiLU prologue on the A operand (results are wrong; variant
+      // builds only, profiles/r4_gn_prologue_probe.txt): scale / shift as lane constants
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        float f[8];
+        unpack8(__builtin_bit_cast(uint4, af[j]), f);
+        const float sc = 1.f + 0.001f * (lane & 7), sh = 0.01f * (lane >> 3);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], sc, sh));
+        af[j] = as_bf16x8(pack8(f));
+      }
+#endif
       // raised wave priority while issuing the MFMA cluster (guide T5): with 2 blocks per CU the
       // wave that has MFMA work keeps the pipe busy while the other waits on its LDS-DMA
       // (+1..13 % on the SD convs / GEMMs, profiles/r1_ops_setprio_ab.txt)

@@ -60,12 +60,27 @@ constexpr size_t pp_lds_bytes() {
   return st > ep ? st : ep;
 }
 
+// DIAG bit 2 probe: x -> silu(x * s + t) on one 8-element A fragment (s, t lane constants)
+CM_DEVICE bf16x8_t gn_silu_probe(bf16x8_t a, int lane) {
+  float f[8];
+  unpack8(__builtin_bit_cast(uint4, a), f);
+  const float sc = 1.f + 0.001f * (lane & 7), sh = 0.01f * (lane >> 3);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], sc, sh));
+  return as_bf16x8(pack8(f));
+}
+
+#ifndef PP_DIAG_DEFAULT
+#define PP_DIAG_DEFAULT 0
+#endif
+
 // SCHED: 0 = four quadrant phases per k-tile (J0 loads W-a and A-a), 1 = four phases with the
 // W-a load moved to J3 of the previous k-tile, 2 = two phases per k-tile (W-a x A, W-b x A).
 // (Reading the next phase's fragments inside the current MFMA cluster was tried: slower on every
 // tile, and the early half would read parts the late half has not waited for; profiles/r2_ppdiag_sched3.jsonl.)
 // DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
-// DMA, bit 1 its barriers
+// DMA, bit 1 its barriers, bit 2 adds a GroupNorm+SiLU cost probe on the A fragments (variant
+// builds with -DPP_DIAG_DEFAULT=4, profiles/r4_gn_prologue_probe.txt)
 template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __restrict__ partial) {
   constexpr bool SPREAD = SCHED == 1;
@@ -442,6 +457,18 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
       wait_vmcnt<0>();
     }
     wait_lgkm<0>();
+    if constexpr ((DIAG & 4) && P == 0) {
+      // cost probe of a GroupNorm+SiLU prologue on the A operand (results are wrong): every A
+      // fragment read this k-tile is normalised and SiLU'd in registers before its MFMAs (the
+      // per-channel scale / shift as lane constants: a LOWER bound of the fused prologue's VALU)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < TJa; ++j) afa[j][ks] = gn_silu_probe(afa[j][ks], lane);
+#pragma unroll
+        for (int j = 0; j < TJb; ++j) afb[j][ks] = gn_silu_probe(afb[j][ks], lane);
+      }
+    }
     if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -512,7 +539,7 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   // the two-phase schedule (SCHED 2; 593 -> 573 ms/step, commit 88fbe5c).  SCHED 0 / 1 are no
   // longer instantiated in the library (tools/ppdiag.hip still builds them for diagnostics)
-  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2>;
+  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, PP_DIAG_DEFAULT>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
