@@ -73,7 +73,8 @@ CM_DEVICE void add4(float* o, uint2 v) {
 
 // folded LayerNorm (p.ln_rows, or p.ln_rows_fx from a producer epilogue): o = rstd_m * (acc -
 // mean_m * wsum[n..n+3]) for the W rows n..n+3
-CM_DEVICE float2 ln_row(const GemmArgs& p, int m) {
+// inv_k = 1 / K (callers hoist it: an fp64 division per row was a ~20-instruction sequence)
+CM_DEVICE float2 ln_row(const GemmArgs& p, int m, double inv_k) {
   if (p.ln_rows_fx != nullptr) {
     // the fixed-point sums are exact; mean and var = q / K - mean^2 are formed in fp64, so rows
     // with |mean| >> std keep their variance (fp32 lost ~log2(mean^2 / var) bits of it to the
@@ -81,9 +82,8 @@ CM_DEVICE float2 ln_row(const GemmArgs& p, int m) {
     // column form of round 3 pushed the 256x256 ping-pong tiles into scratch;
     // tests/test_kernel_registers.py guards it)
     const longlong2 v = reinterpret_cast<const longlong2*>(p.ln_rows_fx)[m];
-    const double inv = 1.0 / (double)p.K;
-    const double mean = (double)v.x * (inv * (1.0 / STAT_SCALE_SUM));
-    const double var = fmax((double)v.y * (inv * (1.0 / STAT_SCALE_SQ)) - mean * mean, 0.0);
+    const double mean = (double)v.x * (inv_k * (1.0 / STAT_SCALE_SUM));
+    const double var = fmax((double)v.y * (inv_k * (1.0 / STAT_SCALE_SQ)) - mean * mean, 0.0);
     return make_float2((float)mean, rsqrtf((float)var + p.ln_eps));
   }
   return reinterpret_cast<const float2*>(p.ln_rows)[m];
@@ -93,7 +93,7 @@ CM_DEVICE void ln_apply4(float2 ms, const float* __restrict__ wsum, float* o) {
   for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, wsum[r], o[r]);
 }
 CM_DEVICE void ln_fold4(const GemmArgs& p, int m, int wn, float* o) {
-  const float2 ms = ln_row(p, m);
+  const float2 ms = ln_row(p, m, 1.0 / (double)p.K);
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] = ms.y * fmaf(-ms.x, p.ln_wsum[wn + r], o[r]);
 }
@@ -203,6 +203,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
       __syncthreads();                        // every wave is done with the staging buffers
       uint16_t* T = reinterpret_cast<uint16_t*>(smem);
       const int hw = p.Ho * p.Wo;
+      const double inv_k = 1.0 / (double)p.K;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int ml = wm * (BM / WM) + 16 * j + fr;
@@ -210,7 +211,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         const int bimg = (p.chan_bias != nullptr && m < p.M) ? (m / hw) : 0;
         // folded LayerNorm: this row's (mean, rstd), once per row (not per 4-column group)
         const bool lnf = (p.ln_rows != nullptr || p.ln_rows_fx != nullptr) && m < p.M;
-        const float2 lnm = lnf ? ln_row(p, m) : make_float2(0.f, 1.f);
+        const float2 lnm = lnf ? ln_row(p, m, inv_k) : make_float2(0.f, 1.f);
         if constexpr (GEGLU) {
 #pragma unroll
           for (int pi = 0; pi < TI / 2; ++pi) {
