@@ -262,6 +262,9 @@ def main() -> int:
         dist.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
+    from cassmantle_amd.utils.tracing import TRACER
+    TRACER.flush()
+    TRACER.reset()                      # stage means over the timed generations only
     t0 = time.perf_counter()
     for k in range(args.steps):
         img = one_step(args.warmup + k)
@@ -273,6 +276,9 @@ def main() -> int:
         torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     mine = elapsed
+    TRACER.flush()
+    stage_ms = {k: v["mean_ms"] for k, v in TRACER.snapshot().items()
+                if k in ("encode", "denoise", "decode")}
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -305,10 +311,6 @@ def main() -> int:
     if rank == 0 and not args.no_score:
         score = scorer_bench(device)    # noqa: F841 - reported below
 
-    from cassmantle_amd.utils.tracing import TRACER
-    TRACER.flush()
-    stage_ms = {k: v["mean_ms"] for k, v in TRACER.snapshot().items()
-                if k in ("encode", "denoise", "decode")}
 
     if rank == 0:
         images = world * args.batch * args.steps
@@ -337,7 +339,7 @@ def main() -> int:
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
             "batch1_s_per_image": b1,       # one room, one image, prompt -> host uint8
             "stage_overlap": sd.decode_stream is not None,
-            "stage_mean_ms": stage_ms,      # device time per generation (incl. warmup)
+            "stage_mean_ms": stage_ms,      # device time per timed generation
             **score,
         }
         if per_rank is not None:
