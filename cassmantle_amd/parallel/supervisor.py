@@ -425,7 +425,11 @@ class GroupSupervisor:
                 break
             batch = [item]
             t_end = time.monotonic() + self.window
+            every_room = set(self.room_ids)
             while True:
+                # a room submits one request per round: once every room is in, the window closes
+                if every_room and {b[0] for b in batch} >= every_room:
+                    break
                 rem = t_end - time.monotonic()
                 if rem <= 0:
                     break
