@@ -73,20 +73,13 @@ CM_DEVICE bf16x8_t gn_silu_probe(bf16x8_t a, int lane) {
 #ifndef PP_DIAG_DEFAULT
 #define PP_DIAG_DEFAULT 0
 #endif
-// library schedule (2 or 3) and, for 3, where in the MFMA cluster the LDS-DMA parts issue
-// (0: before its first MFMA, 1: between its two k-steps)
-#ifndef PP_SCHED_DEFAULT
-#define PP_SCHED_DEFAULT 2
-#endif
-#ifndef PP_S3_POS
-#define PP_S3_POS 1
-#endif
 
 // SCHED: 0 = four quadrant phases per k-tile (J0 loads W-a and A-a), 1 = four phases with the
-// W-a load moved to J3 of the previous k-tile, 2 = two phases per k-tile (W-a x A, W-b x A),
-// 3 = SCHED 2 with the LDS-DMA parts issued inside the MFMA clusters instead of the load segments.
+// W-a load moved to J3 of the previous k-tile, 2 = two phases per k-tile (W-a x A, W-b x A).
 // (Reading the next phase's fragments inside the current MFMA cluster was tried: slower on every
 // tile, and the early half would read parts the late half has not waited for; profiles/r2_ppdiag_sched3.jsonl.)
+// (Issuing the LDS-DMA parts inside the MFMA clusters instead of the load segments was tried in
+// round 4: 3-11 % slower on every conv, profiles/r4_pp_sched3_ab.txt.)
 // DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
 // DMA, bit 1 its barriers, bit 2 adds a GroupNorm+SiLU cost probe on the A fragments (variant
 // builds with -DPP_DIAG_DEFAULT=4, profiles/r4_gn_prologue_probe.txt)
@@ -452,29 +445,17 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
         for (int i = 0; i < TIb; ++i) wfb[i][ks] = as_bf16x8(Bs[wbase_b + 128 * i + lo[ks]]);
     }
     const int u = t + (P == 0 ? 1 : 2);
-    const bool iss = !(DIAG & 1) && u < nk;
-    auto issue = [&]() {
+    if (!(DIAG & 1) && u < nk) {
       if constexpr (P == 0) {
         stage(I1{}, kt0 + u, B ^ 1);
         stage(I3{}, kt0 + u, B ^ 1);
+        wait_vmcnt<G::NR1 + G::NR3>();
       } else {
         stage(I0{}, kt0 + u, B);
         stage(I2{}, kt0 + u, B);
+        wait_vmcnt<G::NR0 + G::NR2>();
       }
-    };
-    if constexpr (SCHED == 2) {
-      if (iss) {
-        issue();
-        if constexpr (P == 0) wait_vmcnt<G::NR1 + G::NR3>();
-        else wait_vmcnt<G::NR0 + G::NR2>();
-      } else {
-        wait_vmcnt<0>();
-      }
-    } else if constexpr (P == 1) {
-      // SCHED 3: the parts are issued inside the MFMA clusters (below), after the barrier that
-      // ends the last read of the bytes they overwrite.  Tile t+1 (W parts from this k-tile's P0
-      // cluster, A parts from the previous P1 cluster) lands before this phase's barrier: the
-      // early half reads it right after the NEXT barrier (this phase's closing one)
+    } else {
       wait_vmcnt<0>();
     }
     wait_lgkm<0>();
@@ -492,14 +473,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
     }
     if constexpr (!(DIAG & 2)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (SCHED == 3 && PP_S3_POS == 0) {
-      if (iss) issue();
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      if constexpr (SCHED == 3 && PP_S3_POS == 1) {
-        if (ks == 1 && iss) issue();
-      }
       if constexpr (P == 0) {
 #pragma unroll
         for (int i = 0; i < TIa; ++i) {
@@ -528,7 +503,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
   };
 
   // two k-tiles per iteration so the buffer of every phase is a compile-time offset
-  if constexpr (SCHED >= 2) {
+  if constexpr (SCHED == 2) {
     for (int t = 0; t < nk; t += 2) {
       mphase(I0{}, I0{}, t);
       mphase(I1{}, I0{}, t);
@@ -566,7 +541,7 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   // the two-phase schedule (SCHED 2; 593 -> 573 ms/step, commit 88fbe5c).  SCHED 0 / 1 are no
   // longer instantiated in the library (tools/ppdiag.hip still builds them for diagnostics)
-  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, PP_SCHED_DEFAULT, PP_DIAG_DEFAULT>;
+  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, PP_DIAG_DEFAULT>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
