@@ -185,9 +185,12 @@ CM_DEVICE void gated_epilogue4_call(const GemmArgs& p, int batch, int m, int n, 
 // statistics); fp32 / split-K / ragged outputs take the direct path.
 // SPLIT_DIRECT: the caller guarantees the direct path only ever stores split-K partial slabs
 // (bf16, N % 8 == 0 outputs always take the LDS path), which keeps the kernel small.
+// has_acc: false for the DMA-only producer waves of a warp-specialised tile (no accumulators;
+// they still take part in the LDS-staged store pass)
 template <int BM, int BN, int WM, int WN, bool GEGLU, bool OUTF32, int TI, int TJ, int THREADS, bool SPLIT_DIRECT = false>
 CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* smem, float* __restrict__ partial,
-                             int m0, int n0, int batch, int wm, int wn, int tid, int nsplit, int split_id) {
+                             int m0, int n0, int batch, int wm, int wn, int tid, int nsplit, int split_id,
+                             bool has_acc = true) {
   const int lane = tid & 63;
   const int fr = lane & 15, fq = lane >> 4;
   // ---- LDS-staged epilogue (bf16 output, no split): the MFMA layout gives each lane 4
@@ -204,6 +207,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
       uint16_t* T = reinterpret_cast<uint16_t*>(smem);
       const int hw = p.Ho * p.Wo;
       const double inv_k = 1.0 / (double)p.K;
+      if (has_acc) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int ml = wm * (BM / WM) + 16 * j + fr;
@@ -249,6 +253,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
             *reinterpret_cast<uint2*>(T + ml * OST + nl) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
           }
         }
+      }
       }
       __syncthreads();
       constexpr int CPR = OBN / 8;              // 16-byte chunks per tile row
@@ -404,6 +409,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
   }
 
   // ---- direct epilogue (fp32 outputs, split-K partial slabs, ragged N)
+  if (!has_acc) return;
   if constexpr (SPLIT_DIRECT) {
     if constexpr (!GEGLU) {
 #pragma unroll
@@ -453,13 +459,21 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
 // keep STAGES-2 k-tiles of DMA in flight across every barrier: the short-K / small-grid UNet
 // GEMMs (K = 320..1280, <= 2 tiles per CU) are bound by the per-k-tile DMA latency, not by
 // MFMA, and a 2-stage loop exposes that latency once per k-tile.
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
-__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 && STAGES == 2) ? 2 : 1)
+//
+// NP > 0 (deep rings only): a warp-specialised block of NW MFMA waves plus NP DMA-only producer
+// waves.  The LDS-DMA fill rate of a CU is set by the waves issuing it (22 / 37 / 48 B/cycle for
+// 4 / 8 / 16 issuing waves, profiles/r3_lds_fill_probe.jsonl), and on the small-grid tiles the MFMA
+// waves also issued the DMA between their fragment reads and MFMAs; with producers the MFMA waves
+// only read LDS and run MFMAs, and the producers only stage (same ring, same barrier per k-tile).
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
+__global__ void __launch_bounds__(64 * (WM * WN + NP), (WM * WN == 4 && STAGES == 2 && NP == 0) ? 2 : 1)
 gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int NW = WM * WN;
-  constexpr int THREADS = 64 * NW;
-  constexpr int RR = 8 * NW;               // rows covered by one DMA round (8 per wave)
+  constexpr int THREADS = 64 * (NW + NP);
+  constexpr int NSW = NP ? NP : NW;        // staging waves
+  static_assert(NP == 0 || (STAGES >= 3 && BUF), "producer waves: buffer-resource deep rings only");
+  constexpr int RR = 8 * NSW;              // rows covered by one DMA round (8 per staging wave)
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int TI = BN / WN / 16;         // n-subtiles per wave
@@ -475,6 +489,9 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int wm = wave % WM, wn = wave / WM;
+  const bool mma_wave = NP == 0 || wave < NW;                  // has accumulators / runs MFMAs
+  const bool dma_wave = NP == 0 || wave >= NW;                 // stages k-tiles
+  const int swave = NP ? (dma_wave ? wave - NW : 0) : wave;    // index among the staging waves
 
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -491,8 +508,8 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
 
   // ---- this lane's DMA rows: round i covers rows 32i + 8*wave + (lane>>3), slot lane&7
   const int slot = lane & 7;
-  const int rsub = 8 * wave + (lane >> 3);
-  const bool w_last_round = (RR * (WR - 1) + 8 * wave) < BN;   // this wave stages the last W round
+  const int rsub = 8 * swave + (lane >> 3);
+  const bool w_last_round = (RR * (WR - 1) + 8 * swave) < BN;  // this wave stages the last W round
   // Per-row state is computed ONCE; the per-k-tile address work is then a few VALU ops per DMA
   // (the first version recomputed divisions per tile and was issue-bound on SALU/VALU:
   // 15 SALU + 9 VALU per MFMA in the rocprof counters).
@@ -631,23 +648,23 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
       if constexpr (CONV == 0) {
         if (p.A2 != nullptr && k0 >= p.ka) {        // wave-uniform: this k-tile lies in A2
 #pragma unroll
-          for (int i = 0; i < AR; ++i) blds16(rsA2, As + (RR * i + 8 * wave) * 8, a_vo2[i], (k0 - p.ka) * 2);
+          for (int i = 0; i < AR; ++i) blds16(rsA2, As + (RR * i + 8 * swave) * 8, a_vo2[i], (k0 - p.ka) * 2);
         } else {
 #pragma unroll
-          for (int i = 0; i < AR; ++i) blds16(rsA, As + (RR * i + 8 * wave) * 8, a_vo[i], soffA);
+          for (int i = 0; i < AR; ++i) blds16(rsA, As + (RR * i + 8 * swave) * 8, a_vo[i], soffA);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
           int vo = a_vo[i];
           if constexpr (CONV == 2) vo = ((a_mask[i] >> tap) & 1) ? vo : (int)0x80000000;
-          blds16(rsA, As + (RR * i + 8 * wave) * 8, vo, soffA);
+          blds16(rsA, As + (RR * i + 8 * swave) * 8, vo, soffA);
         }
       }
 #pragma unroll
       for (int i = 0; i < WR; ++i) {
-        if (RR * i + 8 * wave < BN)
-          blds16(rsW, Ws + (RR * i + 8 * wave) * 8, w_vo[i], k0 * 2);
+        if (RR * i + 8 * swave < BN)
+          blds16(rsW, Ws + (RR * i + 8 * swave) * 8, w_vo[i], k0 * 2);
       }
       if constexpr (CONV >= 2) tap_next();
       return;
@@ -681,13 +698,13 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
           src = A + (((long long)cbh_[i] + iy) * p.IW + ix) * p.Cin + t_ci + a_chunk[i] * 8;
         }
       }
-      glds16(src, As + (RR * i + 8 * wave) * 8);
+      glds16(src, As + (RR * i + 8 * swave) * 8);
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      if (RR * i + 8 * wave < BN) {          // wave-uniform
+      if (RR * i + 8 * swave < BN) {          // wave-uniform
         const void* src = (w_row[i] >= 0 && (kin || k0 + w_chunk[i] * 8 < p.K)) ? (const void*)(W + w_off[i] + k0) : zp;
-        glds16(src, Ws + (RR * i + 8 * wave) * 8);
+        glds16(src, Ws + (RR * i + 8 * swave) * 8);
       }
     }
     if constexpr (CONV >= 2) tap_next();
@@ -783,20 +800,22 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         else wait_vmcnt<3 * (NPT - 1)>();
       }
     };
+    if (dma_wave) {
 #pragma unroll
-    for (int s0 = 0; s0 < S - 1; ++s0)
-      if (s0 < nk) stage(kt0 + s0, s0);
+      for (int s0 = 0; s0 < S - 1; ++s0)
+        if (s0 < nk) stage(kt0 + s0, s0);
+    }
     for (int t = 0; t < nk; ++t) {
-      wait_tiles(min(S - 2, nk - 1 - t));
+      if (dma_wave) wait_tiles(min(S - 2, nk - 1 - t));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();        // every wave's share of tile t landed; tile t-1 is free
-      if (t + S - 1 < nk) stage(kt0 + t + S - 1, (t + S - 1) % S);
-      compute(t % S);
+      if (dma_wave && t + S - 1 < nk) stage(kt0 + t + S - 1, (t + S - 1) % S);
+      if (mma_wave) compute(t % S);
     }
   }
 
   tile_epilogue<BM, BN, WM, WN, GEGLU, OUTF32, TI, TJ, THREADS>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
-                                                               gridDim.y, blockIdx.y);
+                                                               gridDim.y, blockIdx.y, mma_wave);
 }
 
 // split-K: a second, fully parallel pass sums the slices' fp32 slabs and applies the epilogue
@@ -925,7 +944,7 @@ void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
 void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -936,7 +955,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = lds_stage > lds_epi ? lds_stage : lds_epi;
   // (the kernel is named once, outside any lambda: a kernel template referenced only from a
   // lambda inside this function template was left uninstantiated by hipcc)
-  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF>;
+  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, NP>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
     // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
@@ -946,7 +965,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
     }();
     (void)once;
   }
-  hipLaunchKernelGGL(kfn, grid, dim3(64 * WM * WN), lds, s, p, ws);
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * (WM * WN + NP)), lds, s, p, ws);
   if (split > 1) launch_splitk_reduce<OUTF32>(p, ws, split, s);
 }
 
@@ -972,6 +991,10 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 16: return launch_t<128, 80, 4, 1, CONV, false, false, 4, true>(p, ws, s);
       case 26: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true>(p, ws, s);
       case 27: return launch_t<128, 64, 4, 2, CONV, false, false, 3, true>(p, ws, s);
+      // warp-specialised: 8 MFMA waves + 8 DMA-only producer waves (1024 threads)
+      case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
+      case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
+      case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       default: break;
     }
   }
