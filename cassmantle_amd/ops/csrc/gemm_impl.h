@@ -995,6 +995,9 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
       case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
+      case 34: return launch_t<256, 128, 4, 2, CONV, false, false, 3, true, 8>(p, ws, s);
+      case 35: return launch_t<128, 256, 2, 4, CONV, false, false, 3, true, 8>(p, ws, s);
+      case 36: return launch_t<128, 128, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       default: break;
     }
   }
