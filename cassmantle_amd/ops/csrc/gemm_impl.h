@@ -995,9 +995,8 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
       case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
-      case 34: return launch_t<128, 160, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
-      // (256x128 / 128x256 / 128x128 producer-wave tiles were tuned in situ in round 4: 8 of the
-      // SD-1.5 / SDXL shapes, bench neutral; removed, profiles/r4_producer_waves_ab.txt)
+      // (256x128 / 128x256 / 128x128 and 128x160 8x1 (also gated) producer-wave tiles were tuned
+      // in situ in round 4: bench-neutral, removed; profiles/r4_producer_waves_ab.txt)
       default: break;
     }
   }
@@ -1017,9 +1016,6 @@ void launch_tiles(const GemmArgs& p, float* ws, hipStream_t s) {
   if (p.act == ACT_GEGLU || p.act == ACT_SWIGLU) {
     if constexpr (BUF) {
       if (p.cfg == 12) return launch_t<128, 128, 2, 2, CONV, true, false, 4, true>(p, ws, s);
-      // warp-specialised gated tile: 8 MFMA waves stacked along M (wave tile 16 x 160: 5
-      // value/gate pairs, 80 outputs per block) + 8 producer waves
-      if (p.cfg == 34) return launch_t<128, 160, 8, 1, CONV, true, false, 4, true, 8>(p, ws, s);
     }
     if (p.cfg == 6) launch_st<256, 128, 4, 2, CONV, true, false, BUF>(p, ws, s);
     else launch_st<128, 128, 2, 2, CONV, true, false, BUF>(p, ws, s);
