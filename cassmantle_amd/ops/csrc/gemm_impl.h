@@ -482,7 +482,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   static_assert(BM % RR == 0, "A rows in whole DMA rounds");
   constexpr int AR = BM / RR;              // A DMA rounds
   constexpr int WR = (BN + RR - 1) / RR;   // W DMA rounds (the last may cover only some waves)
-  static_assert(STAGES >= 2 && STAGES <= 5, "stages");
+  static_assert(STAGES >= 2 && STAGES <= 6, "stages");
   constexpr int NPT = AR + WR;             // DMA instructions per k-tile of a wave in every round
 
   const int tid = threadIdx.x;
@@ -792,12 +792,14 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         if (k <= 0) wait_vmcnt<0>();
         else if (k == 1) wait_vmcnt<NPT>();
         else if (k == 2) wait_vmcnt<2 * NPT>();
-        else wait_vmcnt<3 * NPT>();
+        else if (k == 3 || S < 6) wait_vmcnt<3 * NPT>();
+        else wait_vmcnt<4 * NPT>();
       } else {
         if (k <= 0) wait_vmcnt<0>();
         else if (k == 1) wait_vmcnt<NPT - 1>();
         else if (k == 2) wait_vmcnt<2 * (NPT - 1)>();
-        else wait_vmcnt<3 * (NPT - 1)>();
+        else if (k == 3 || S < 6) wait_vmcnt<3 * (NPT - 1)>();
+        else wait_vmcnt<4 * (NPT - 1)>();
       }
     };
     if (dma_wave) {
@@ -995,6 +997,10 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
       case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
+      // 6-stage producer-wave rings: 4 k-tiles of LDS-DMA in flight for weight-streaming GEMMs whose
+      // weights come from HBM on every call (a UNet eval reads each weight once)
+      case 34: return launch_t<128, 80, 8, 1, CONV, false, false, 6, true, 8>(p, ws, s);
+      case 35: return launch_t<128, 64, 4, 2, CONV, false, false, 6, true, 8>(p, ws, s);
       // (256x128 / 128x256 / 128x128 and 128x160 8x1 (also gated) producer-wave tiles were tuned
       // in situ in round 4: bench-neutral, removed; profiles/r4_producer_waves_ab.txt)
       default: break;
