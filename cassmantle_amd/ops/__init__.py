@@ -93,7 +93,9 @@ def _launch(fn, *args, **kw):
         load_gemm_tuning()
     fn(*args, **kw)
     if _RECORD is not None:
-        _RECORD.append((ext().gemm_last_key(), lambda: fn(*args, **kw)))
+        call = lambda: fn(*args, **kw)   # noqa: E731
+        call.fn, call.args, call.kw = fn, args, kw    # (tools/autotune_gemm.py --cold swaps the weight)
+        _RECORD.append((ext().gemm_last_key(), call))
 
 
 _ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "quick_gelu": 3, "geglu": 4, "gelu_tanh": 5, "swiglu": 6}

@@ -45,6 +45,34 @@ def timeit(fn, iters):
     return e0.elapsed_time(e1) / iters * 1e3
 
 
+def weight_rotation(key: str, call, mib: int):
+    """-> a closure that re-launches ``call`` with the next of R copies of its weight each time
+    (R x |W| >= ``mib`` MiB: every call reads its weight from HBM, as a UNet eval does), or None
+    when the weight argument cannot be identified.  The weight is the bf16 tensor argument with
+    Nw x K elements (key fields w / k) that is not the first tensor argument (the activations)."""
+    f = dict(t[:1] and (t[0], t[1:]) for t in key.split() if t[:1] in "wk" and t[1:].lstrip("-").isdigit())
+    if "w" not in f or "k" not in f or not hasattr(call, "args"):
+        return None
+    numel = int(f["w"]) * int(f["k"])
+    tens = [i for i, v in enumerate(call.args) if torch.is_tensor(v)]
+    cand = [i for i in tens[1:] if call.args[i].dtype == torch.bfloat16 and call.args[i].numel() == numel]
+    if len(cand) != 1:
+        return None
+    wi = cand[0]
+    w = call.args[wi]
+    reps = max(2, min(512, (mib << 20) // max(1, w.numel() * 2) + 1))
+    copies = [w.clone() for _ in range(reps)]
+    state = {"i": 0}
+
+    def run():
+        args = list(call.args)
+        args[wi] = copies[state["i"] % reps]
+        state["i"] += 1
+        call.fn(*args, **call.kw)
+    run.copies = copies
+    return run
+
+
 def record_pass(model: str, batch: int):
     from cassmantle_amd.pipeline import SPECS, StableDiffusion
     from cassmantle_amd.models.schedulers import make_plan
@@ -78,6 +106,10 @@ def main():
     ap.add_argument("--cfgs", default=None,
                     help="comma list of tile configs to time (default: all); with --merge the shape's "
                          "existing table plan is always an arm, so a partial sweep only adds new winners")
+    ap.add_argument("--cold", type=int, default=0, metavar="MIB",
+                    help="time every arm with its weight read from HBM on each call (rotating over "
+                         "copies totalling MIB MiB, e.g. 512 = twice the Infinity Cache), as in a "
+                         "UNet eval; 0 = warm (the same weight tensor re-run)")
     a = ap.parse_args()
     cfgs = [int(c) for c in a.cfgs.split(",")] if a.cfgs else CFGS
     os.environ["CASSMANTLE_GEMM_TUNE"] = "0"
@@ -115,16 +147,18 @@ def main():
                     arms.setdefault(pl, f"{c}/{sp}")
             ext().gemm_set_override(-1, 0)
             auto_plan = next(k for k, v in arms.items() if v == "auto")
+            run = weight_rotation(key, fn, a.cold) if a.cold else None
             res = {pl: [] for pl in arms}
             for _ in range(a.rounds):
                 for pl in arms:
                     ext().gemm_set_override(pl[0], pl[1])
-                    res[pl].append(timeit(fn, a.iters))
+                    res[pl].append(timeit(run or fn, a.iters))
             ext().gemm_set_override(-1, 0)
+            del run
             med = {pl: statistics.median(v) for pl, v in res.items()}
             best = min(med, key=med.get)
             gain = med[auto_plan] / med[best]
-            line = {"key": key, "calls_per_pass": counts[key], "auto": list(auto_plan),
+            line = {"key": key, "cold": bool(a.cold), "calls_per_pass": counts[key], "auto": list(auto_plan),
                     "auto_us": round(med[auto_plan], 2), "best": list(best), "best_us": round(med[best], 2),
                     "gain": round(gain, 3), "arms": len(arms)}
             print(json.dumps(line), flush=True)
