@@ -465,13 +465,17 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
 // 4 / 8 / 16 issuing waves, profiles/r3_lds_fill_probe.jsonl), and on the small-grid tiles the MFMA
 // waves also issued the DMA between their fragment reads and MFMAs; with producers the MFMA waves
 // only read LDS and run MFMAs, and the producers only stage (same ring, same barrier per k-tile).
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
+// MIX: the MFMA waves stage too (every wave issues LDS-DMA, the producers only that): 16 issuing
+// waves fill at ~48 B/cycle/CU against ~37 for 8, and the MFMA waves of a small tile idle for most
+// of a fill-bound k-tile anyway
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0,
+          bool MIX = false>
 __global__ void __launch_bounds__(64 * (WM * WN + NP), (WM * WN == 4 && STAGES == 2 && NP == 0) ? 2 : 1)
 gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int NW = WM * WN;
   constexpr int THREADS = 64 * (NW + NP);
-  constexpr int NSW = NP ? NP : NW;        // staging waves
+  constexpr int NSW = NP ? (MIX ? NP + NW : NP) : NW;   // staging waves
   static_assert(NP == 0 || (STAGES >= 3 && BUF), "producer waves: buffer-resource deep rings only");
   constexpr int RR = 8 * NSW;              // rows covered by one DMA round (8 per staging wave)
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
@@ -490,8 +494,10 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int wm = wave % WM, wn = wave / WM;
   const bool mma_wave = NP == 0 || wave < NW;                  // has accumulators / runs MFMAs
-  const bool dma_wave = NP == 0 || wave >= NW;                 // stages k-tiles
-  const int swave = NP ? (dma_wave ? wave - NW : 0) : wave;    // index among the staging waves
+  const bool dma_wave = NP == 0 || MIX || wave >= NW;          // stages k-tiles
+  // index among the staging waves (MIX: producers first, so the partial last W round -- the
+  // extra DMA some waves issue -- falls on producers before MFMA waves)
+  const int swave = NP ? (wave >= NW ? wave - NW : (MIX ? wave + NP : 0)) : wave;
 
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -946,7 +952,8 @@ void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0,
+          bool MIX = false>
 void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -957,7 +964,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = lds_stage > lds_epi ? lds_stage : lds_epi;
   // (the kernel is named once, outside any lambda: a kernel template referenced only from a
   // lambda inside this function template was left uninstantiated by hipcc)
-  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, NP>;
+  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, NP, MIX>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
     // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
@@ -997,6 +1004,10 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
       case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
+      // the same three with the MFMA waves staging too (16 issuing waves)
+      case 34: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8, true>(p, ws, s);
+      case 35: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8, true>(p, ws, s);
+      case 36: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8, true>(p, ws, s);
       // (256x128 / 128x256 / 128x128 and 128x160 8x1 (also gated) producer-wave tiles were tuned
       // in situ in round 4: bench-neutral, removed; profiles/r4_producer_waves_ab.txt.  6-stage
       // rings of 31 / 32: no faster with weights from HBM on every call,
