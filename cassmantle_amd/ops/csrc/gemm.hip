@@ -47,7 +47,6 @@ constexpr int BK = 64;
 //       threads, 4 stages): 128x80 (8x1), 128x64 (4x2), 128x160 (4x2).  (256x128 / 128x256 / 128x128
 //       and the gated 128x160 8x1 producer-wave tiles: bench-neutral in situ, removed;
 //       profiles/r4_producer_waves_ab.txt)
-//   34 / 35 / 36: 31 / 32 / 33 with the MFMA waves staging too (all 16 waves issue LDS-DMA)
 // Removed in round 4 (measured, picked by no shape of the SD-1.5 / SDXL census; results kept in
 // profiles/ and in git history): 11 (128x160 4w S4), 17-19 (register-staged 4-wave tiles,
 // profiles/r2_regstage_ab.txt), 23 (ping-pong 256x64), 24/25 (halo-staged 3x3 conv,
@@ -56,14 +55,14 @@ constexpr int BK = 64;
 // profiles/r3_tune_8wave_gated.txt).  Their indices stay reserved so table keys keep their meaning.
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
-constexpr int kNumTiles = 37;
+constexpr int kNumTiles = 34;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
 constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22; }
 // configs with a kernel behind them (the reserved indices above have none)
 constexpr bool is_live_cfg(int c) {
   return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 22) || c == 26 || c == 27 ||
-         (c >= 31 && c <= 36);
+         (c >= 31 && c <= 33);
 }
 constexpr int kAreg = 15;
 constexpr int kFirstPP = 7;
@@ -82,7 +81,6 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {256, 160, 1.f, 256},   {128, 160, 1.f, 256},   {128, 80, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 64, 1.f, 256},    {128, 128, 1.f, 256},
                                        {256, 80, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 256},
-                                       {128, 160, 1.f, 256},   {128, 80, 1.f, 256},    {128, 64, 1.f, 256},
                                        {128, 160, 1.f, 256}};
 
 // buffer-resource LDS-DMA path: K in whole k-tiles and every byte range addressable by a

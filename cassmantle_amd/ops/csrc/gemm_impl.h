@@ -1004,14 +1004,11 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       case 31: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8>(p, ws, s);
       case 32: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
       case 33: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8>(p, ws, s);
-      // the same three with the MFMA waves staging too (16 issuing waves)
-      case 34: return launch_t<128, 80, 8, 1, CONV, false, false, 4, true, 8, true>(p, ws, s);
-      case 35: return launch_t<128, 64, 4, 2, CONV, false, false, 4, true, 8, true>(p, ws, s);
-      case 36: return launch_t<128, 160, 4, 2, CONV, false, false, 4, true, 8, true>(p, ws, s);
       // (256x128 / 128x256 / 128x128 and 128x160 8x1 (also gated) producer-wave tiles were tuned
       // in situ in round 4: bench-neutral, removed; profiles/r4_producer_waves_ab.txt.  6-stage
       // rings of 31 / 32: no faster with weights from HBM on every call,
-      // profiles/r4_cold_weight_probe.jsonl)
+      // profiles/r4_cold_weight_probe.jsonl.  31-33 with the MFMA waves staging too (MIX): 3-15 %
+      // slower per call, bench-neutral, profiles/r4_producer_waves_ab.txt)
       default: break;
     }
   }

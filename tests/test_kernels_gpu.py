@@ -253,7 +253,7 @@ def test_layer_norm_folded_into_gemm(rows, K, N, act, res):
     assert rel_err(out, exp) < 1.5e-2
 
 
-@pytest.mark.parametrize("cfg", [31, 33, 34, 36])
+@pytest.mark.parametrize("cfg", [31, 33])
 def test_layer_norm_folded_into_producer_wave_gemm(cfg, force_cfg):
     """the level-3 projection shape on the warp-specialised tiles (8 MFMA + 8 producer waves):
     folded LayerNorm epilogue (row statistics + wsum correction); the gated call forced onto a
@@ -526,7 +526,7 @@ def test_latent_step_matches_reference(sched):
 
 
 # ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
-PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 26, 27, 31, 32, 33, 34, 35, 36]   # ping-pong (7-10, 20-22), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-36)
+PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 26, 27, 31, 32, 33]   # ping-pong (7-10, 20-22), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-33)
 
 
 @pytest.fixture
