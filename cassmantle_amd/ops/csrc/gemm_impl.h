@@ -465,17 +465,13 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
 // 4 / 8 / 16 issuing waves, profiles/r3_lds_fill_probe.jsonl), and on the small-grid tiles the MFMA
 // waves also issued the DMA between their fragment reads and MFMAs; with producers the MFMA waves
 // only read LDS and run MFMAs, and the producers only stage (same ring, same barrier per k-tile).
-// MIX: the MFMA waves stage too (every wave issues LDS-DMA, the producers only that): 16 issuing
-// waves fill at ~48 B/cycle/CU against ~37 for 8, and the MFMA waves of a small tile idle for most
-// of a fill-bound k-tile anyway
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0,
-          bool MIX = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
 __global__ void __launch_bounds__(64 * (WM * WN + NP), (WM * WN == 4 && STAGES == 2 && NP == 0) ? 2 : 1)
 gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int NW = WM * WN;
   constexpr int THREADS = 64 * (NW + NP);
-  constexpr int NSW = NP ? (MIX ? NP + NW : NP) : NW;   // staging waves
+  constexpr int NSW = NP ? NP : NW;        // staging waves
   static_assert(NP == 0 || (STAGES >= 3 && BUF), "producer waves: buffer-resource deep rings only");
   constexpr int RR = 8 * NSW;              // rows covered by one DMA round (8 per staging wave)
   constexpr int TILE = (BM + BN) * 8;      // uint4 per buffer
@@ -486,7 +482,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   static_assert(BM % RR == 0, "A rows in whole DMA rounds");
   constexpr int AR = BM / RR;              // A DMA rounds
   constexpr int WR = (BN + RR - 1) / RR;   // W DMA rounds (the last may cover only some waves)
-  static_assert(STAGES >= 2 && STAGES <= 6, "stages");
+  static_assert(STAGES >= 2 && STAGES <= 5, "stages");
   constexpr int NPT = AR + WR;             // DMA instructions per k-tile of a wave in every round
 
   const int tid = threadIdx.x;
@@ -494,10 +490,8 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int wm = wave % WM, wn = wave / WM;
   const bool mma_wave = NP == 0 || wave < NW;                  // has accumulators / runs MFMAs
-  const bool dma_wave = NP == 0 || MIX || wave >= NW;          // stages k-tiles
-  // index among the staging waves (MIX: producers first, so the partial last W round -- the
-  // extra DMA some waves issue -- falls on producers before MFMA waves)
-  const int swave = NP ? (wave >= NW ? wave - NW : (MIX ? wave + NP : 0)) : wave;
+  const bool dma_wave = NP == 0 || wave >= NW;                 // stages k-tiles
+  const int swave = NP ? (dma_wave ? wave - NW : 0) : wave;    // index among the staging waves
 
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -798,14 +792,12 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
         if (k <= 0) wait_vmcnt<0>();
         else if (k == 1) wait_vmcnt<NPT>();
         else if (k == 2) wait_vmcnt<2 * NPT>();
-        else if (k == 3 || S < 6) wait_vmcnt<3 * NPT>();
-        else wait_vmcnt<4 * NPT>();
+        else wait_vmcnt<3 * NPT>();
       } else {
         if (k <= 0) wait_vmcnt<0>();
         else if (k == 1) wait_vmcnt<NPT - 1>();
         else if (k == 2) wait_vmcnt<2 * (NPT - 1)>();
-        else if (k == 3 || S < 6) wait_vmcnt<3 * (NPT - 1)>();
-        else wait_vmcnt<4 * (NPT - 1)>();
+        else wait_vmcnt<3 * (NPT - 1)>();
       }
     };
     if (dma_wave) {
@@ -952,8 +944,7 @@ void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0,
-          bool MIX = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool OUTF32, int STAGES, bool BUF, int NP = 0>
 void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -964,7 +955,7 @@ void launch_t(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = lds_stage > lds_epi ? lds_stage : lds_epi;
   // (the kernel is named once, outside any lambda: a kernel template referenced only from a
   // lambda inside this function template was left uninstantiated by hipcc)
-  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, NP, MIX>;
+  auto* kfn = &gemm_kernel<BM, BN, WM, WN, CONV, GEGLU, OUTF32, STAGES, BUF, NP>;
   if constexpr (lds > 65536) {
     // > 64 KiB dynamic LDS must be opted into once (first call happens before any graph capture)
     // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
@@ -1007,8 +998,8 @@ void launch_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
       // (256x128 / 128x256 / 128x128 and 128x160 8x1 (also gated) producer-wave tiles were tuned
       // in situ in round 4: bench-neutral, removed; profiles/r4_producer_waves_ab.txt.  6-stage
       // rings of 31 / 32: no faster with weights from HBM on every call,
-      // profiles/r4_cold_weight_probe.jsonl.  31-33 with the MFMA waves staging too (MIX): 3-15 %
-      // slower per call, bench-neutral, profiles/r4_producer_waves_ab.txt)
+      // profiles/r4_cold_weight_probe.jsonl.  31-33 with the MFMA waves staging too: 3-15 % slower
+      // per call, bench-neutral, profiles/r4_producer_waves_ab.txt)
       default: break;
     }
   }
