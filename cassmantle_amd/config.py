@@ -114,6 +114,10 @@ class ModelConfig:
     scorer: str = "minilm"               # minilm | wordvec
     scorer_weights: Optional[str] = None  # BertModel / sentence-transformers MiniLM safetensors
     scorer_batch_window_ms: float = 1.0   # micro-batch window for streaming guess scoring
+    # scorer stream priority (-1 high, 0 normal); None = high when this process also generates, normal
+    # in the supervised front-end, whose GPU-0 neighbour is a worker PROCESS: there a high-priority
+    # scorer cost generation 6 % more at no gain in scoring p99 (profiles/r4_live_topologies.txt)
+    scorer_stream_priority: Optional[int] = None
     # CUs reserved for guess scoring on a GPU that also generates (runtime/cumask.py): the scorer
     # stream runs on these CUs only, the generation stream on the rest (0 = no reservation)
     scorer_reserved_cus: int = 0

@@ -57,8 +57,11 @@ def build_scorer(cfg: Config, device: Optional[str] = None, wrap=None):
         backend = WordVectorBackend(device=dev, dtype=torch.bfloat16 if dev.startswith("cuda") else torch.float32)
     else:
         from ..scoring.encoder import EncoderBackend
-        # high-priority stream: guess scoring is dispatched ahead of queued denoise kernels
-        backend = EncoderBackend(device=dev, stream_priority=-1 if dev.startswith("cuda") else None,
+        # high-priority stream: guess scoring is dispatched ahead of queued denoise kernels (the
+        # supervised front-end sets cfg.model.scorer_stream_priority = 0, serve._serve_supervised)
+        prio = cfg.model.scorer_stream_priority
+        prio = (-1 if prio is None else prio) if dev.startswith("cuda") else None
+        backend = EncoderBackend(device=dev, stream_priority=prio,
                                  dtype=model_dtype(cfg, dev), stream=reserved_streams(cfg, dev)[0])
         if cfg.model.scorer_weights:
             from ..models.weights import load_bert, read_safetensors

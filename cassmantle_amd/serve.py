@@ -137,6 +137,8 @@ def _serve_supervised(cfg, args) -> int:
                           stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s,
                           reprobe_s=cfg.game.device_reprobe_s)
     sup.wait_ready()
+    if cfg.model.scorer_stream_priority is None:
+        cfg.model.scorer_stream_priority = 0      # no generation in this process (config.py)
     svc = build_service(cfg, image_gen_for_room=lambda rid: SupervisedImageGenerator(sup, rid), room_ids=room_ids)
     app = create_app(svc, cfg)
     app.state.supervisor = sup

@@ -52,7 +52,9 @@ def parse():
     ap.add_argument("--think-ms", type=float, default=250.0)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--model", default="sd15")
-    ap.add_argument("--priority", type=int, default=-1, help="scorer stream priority (lower = higher)")
+    ap.add_argument("--priority", type=int, default=None,
+                    help="scorer stream priority (lower = higher); default -1 in-process, 0 in the supervised "
+                         "front-end (as serve.py: config.ModelConfig.scorer_stream_priority)")
     ap.add_argument("--no-priority", action="store_true",
                     help="A/B: score on a normal-priority side stream (the scorer always owns a stream: "
                          "on the legacy default stream it queued behind whole generations, "
@@ -123,7 +125,8 @@ def main_supervised(a) -> None:
     print(f"[live] worker group up on {sup.live_devices()} in {time.perf_counter() - t_start:.1f} s",
           file=sys.stderr, flush=True)
     dev = torch.device("cuda:0" if gpu else "cpu")
-    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority)
+    prio = 0 if a.no_priority else (0 if a.priority is None else a.priority)
+    backend = EncoderBackend(device=str(dev), stream_priority=prio)
     scorer = BatchingScorer(backend, 0.01, window_ms=a.window_ms)
     gen = SyntheticPromptGenerator(salt=0)
     seeds_txt, styles = load_seeds(), load_styles()
@@ -174,7 +177,7 @@ def main_supervised(a) -> None:
         "idle_p50_ms": round(pct(idle, 50), 3), "idle_p99_ms": round(pct(idle, 99), 3),
         "load_p50_ms": round(pct(load, 50), 3), "load_p99_ms": round(pct(load, 99), 3), "requests": len(load),
         "rounds": done["rounds"], "gather_us_p50": st["gather_us_p50"], "retired": st["retired"],
-        "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
+        "scorer_stream_priority": prio, "seconds": a.seconds,
         "config": {"model": a.model, "batch_per_room": a.batch, "rooms": len(rooms)}}), flush=True)
 
 
@@ -198,7 +201,8 @@ def main():
         from cassmantle_amd.runtime.cumask import reserved_streams
         s_score, s_gen = reserved_streams(dev, a.reserve_cus, exclusive=a.exclusive_scorer)
     sd = StableDiffusion(SPECS[a.model], device=dev, seed=0, stream=s_gen)
-    backend = EncoderBackend(device=str(dev), stream_priority=0 if a.no_priority else a.priority, stream=s_score)
+    prio = 0 if a.no_priority else (-1 if a.priority is None else a.priority)
+    backend = EncoderBackend(device=str(dev), stream_priority=prio, stream=s_score)
     sharded = follower = None
     if a.score_topology == "sharded" and world > 1:
         from cassmantle_amd.parallel.scoring import ShardedSimilarity, new_scoring_group
@@ -278,7 +282,7 @@ def main():
             "images_per_s": round(s[0], 3), "n_gpus": world, "players": a.players,
             "think_ms": a.think_ms, "idle_p50_ms": round(s[1], 3), "idle_p99_ms": round(s[2], 3),
             "load_p50_ms": round(s[3], 3), "load_p99_ms": round(s[4], 3), "requests": int(s[5]),
-            "scorer_stream_priority": 0 if a.no_priority else a.priority, "seconds": a.seconds,
+            "scorer_stream_priority": prio, "seconds": a.seconds,
             "score_topology": a.score_topology, "reserved_cus": a.reserve_cus, "exclusive_scorer": a.exclusive_scorer,
             "switch_ms": sys.getswitchinterval() * 1e3,
             "sharded_pairs": sharded.sharded_pairs if sharded is not None else 0,
