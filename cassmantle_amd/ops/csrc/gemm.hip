@@ -39,8 +39,6 @@ constexpr int BK = 64;
 //       (M = 8192 x N = 640: 256 tiles)
 //   21: ping-pong 128x128 (4x2 waves, wave 32x64, 64 KiB LDS: 2 blocks per CU)
 //   22: ping-pong 128x64 (4x2 waves, 48 KiB LDS)
-//   23: gated ping-pong 256x160 on 4x2 waves with interleaved value / gate rows (gemm_pp.h GILV;
-//       gated calls only -- a plain call forced to 23 runs the 256x256 tile)
 //   26 / 27: 8-wave 128x80 (8x1 waves, wave 16x80, 4-stage ring) / 128x64 (4x2 waves, 3 stages):
 //       the small-grid tiles with twice the waves issuing LDS-DMA.  A CU's LDS-DMA fill rate is
 //       set by the number of waves issuing it, not by the bytes in flight (4 waves: 22 B/cycle
@@ -51,7 +49,7 @@ constexpr int BK = 64;
 //       profiles/r4_producer_waves_ab.txt)
 // Removed in round 4 (measured, picked by no shape of the SD-1.5 / SDXL census; results kept in
 // profiles/ and in git history): 11 (128x160 4w S4), 17-19 (register-staged 4-wave tiles,
-// profiles/r2_regstage_ab.txt), 24/25 (halo-staged 3x3 conv,
+// profiles/r2_regstage_ab.txt), 23 (ping-pong 256x64), 24/25 (halo-staged 3x3 conv,
 // profiles/r3_bench_halo.jsonl), 28 (16-wave 128x64, profiles/r3_probe_16wave.jsonl), 29/30 (8-wave
 // 128x128 / 256x80 and the gated 128x128, profiles/r3_tune_8wave_b_ab.txt,
 // profiles/r3_tune_8wave_gated.txt).  Their indices stay reserved so table keys keep their meaning.
@@ -60,10 +58,10 @@ struct TileCfg { int BM, BN; float eff; int slots; };
 constexpr int kNumTiles = 34;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
-constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22 || c == 23; }
+constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22; }
 // configs with a kernel behind them (the reserved indices above have none)
 constexpr bool is_live_cfg(int c) {
-  return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 23) || c == 26 || c == 27 ||
+  return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 22) || c == 26 || c == 27 ||
          (c >= 31 && c <= 33);
 }
 constexpr int kAreg = 15;
@@ -79,7 +77,7 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 768},
                                        {128, 128, 1.f, 512},   {128, 160, 1.f, 512},   {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 160, 1.f, 256},
+                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512},
                                        {256, 160, 1.f, 256},   {128, 160, 1.f, 256},   {128, 80, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 64, 1.f, 256},    {128, 128, 1.f, 256},
                                        {256, 80, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 256},
@@ -280,7 +278,7 @@ static GemmPlan gemm_plan_impl(const GemmArgs& p) {
     if (gated) {
       if (force_cfg == 0 || force_cfg == 6) best.cfg = force_cfg;
       else if (force_cfg >= kFirstDeep) best.cfg = 12;    // the deep-ring gated tile
-      else if (force_cfg >= kFirstPP) best.cfg = (force_cfg == 8 || force_cfg == 23) ? force_cfg : 9;   // the ping-pong gated tiles
+      else if (force_cfg >= kFirstPP) best.cfg = force_cfg == 8 ? 8 : 9;   // the ping-pong gated tiles
       return best;
     }
     only = force_cfg;

@@ -187,8 +187,7 @@ CM_DEVICE void gated_epilogue4_call(const GemmArgs& p, int batch, int m, int n, 
 // (bf16, N % 8 == 0 outputs always take the LDS path), which keeps the kernel small.
 // has_acc: false for the DMA-only producer waves of a warp-specialised tile (no accumulators;
 // they still take part in the LDS-staged store pass)
-template <int BM, int BN, int WM, int WN, bool GEGLU, bool OUTF32, int TI, int TJ, int THREADS, bool SPLIT_DIRECT = false,
-          bool GILV = false>
+template <int BM, int BN, int WM, int WN, bool GEGLU, bool OUTF32, int TI, int TJ, int THREADS, bool SPLIT_DIRECT = false>
 CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* smem, float* __restrict__ partial,
                              int m0, int n0, int batch, int wm, int wn, int tid, int nsplit, int split_id,
                              bool has_acc = true) {
@@ -217,34 +216,7 @@ CM_DEVICE void tile_epilogue(const GemmArgs& p, f32x4_t (&acc)[TI][TJ], uint4* s
         // folded LayerNorm: this row's (mean, rstd), once per row (not per 4-column group)
         const bool lnf = (p.ln_rows != nullptr || p.ln_rows_fx != nullptr) && m < p.M;
         const float2 lnm = lnf ? ln_row(p, m, inv_k) : make_float2(0.f, 1.f);
-        if constexpr (GILV) {
-          // interleaved gates (gemm_pp.h GILV): in every 16-row block i, lanes with fq < 2 hold
-          // the values of outputs 8i + 4 fq + r, lanes fq + 2 (lane ^ 32) their gates.  LayerNorm
-          // and bias are applied per own column, then one permlane32 swap pairs them; the low half
-          // finishes outputs r = 0, 1 and the high half r = 2, 3 of the lane pair
-          const bool hi = lane >= 32;
-#pragma unroll
-          for (int i = 0; i < TI; ++i) {
-            const int nl = wn * (BN / WN / 2) + 8 * i + 4 * (fq & 1);
-            const int n = n0 + nl;
-            const int col = hi ? p.N + n : n;               // this lane's W row (value / gate column)
-            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (lnf && n < p.N) ln_apply4(lnm, p.ln_wsum + col, o);
-            if (p.bias && n < p.N) add4(o, *reinterpret_cast<const uint2*>(p.bias + col));
-            float other[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const unsigned u = __float_as_uint(o[r]);
-              const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-              other[r] = __uint_as_float(hi ? sw[0] : sw[1]);
-            }
-            // (static register indices only: a lane-dependent index would put o / other in scratch)
-            const float h0 = hi ? other[2] : o[0], g0 = hi ? o[2] : other[0];
-            const float h1 = hi ? other[3] : o[1], g1 = hi ? o[3] : other[1];
-            *reinterpret_cast<uint32_t*>(T + ml * OST + nl + (hi ? 2 : 0)) =
-                pack2(gate_f(h0, g0, p.act), gate_f(h1, g1, p.act));
-          }
-        } else if constexpr (GEGLU) {
+        if constexpr (GEGLU) {
 #pragma unroll
           for (int pi = 0; pi < TI / 2; ++pi) {
             const int nl = wn * (BN / WN / 2) + 16 * pi + 4 * fq;

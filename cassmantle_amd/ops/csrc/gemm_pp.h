@@ -80,14 +80,13 @@ CM_DEVICE bf16x8_t gn_silu_probe(bf16x8_t a, int lane) {
 // tile, and the early half would read parts the late half has not waited for; profiles/r2_ppdiag_sched3.jsonl.)
 // (Issuing the LDS-DMA parts inside the MFMA clusters instead of the load segments was tried in
 // round 4: 3-11 % slower on every conv, profiles/r4_pp_sched3_ab.txt.)
+// (A gated 256x160 tile on 4x2 waves -- value / gate rows interleaved at 8-row granularity, paired
+// by v_permlane32_swap in the epilogue -- was correct but no faster than the 8x1 gated tile on the
+// level-3 GEGLU, 68.3 us; round 4, profiles/r4_producer_waves_ab.txt.)
 // DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
 // DMA, bit 1 its barriers, bit 2 adds a GroupNorm+SiLU cost probe on the A fragments (variant
 // builds with -DPP_DIAG_DEFAULT=4, profiles/r4_gn_prologue_probe.txt)
-// GILV (gated only): value and gate rows interleaved at 8-row granularity inside every 16-row
-// MFMA block (rows 0-7 values, 8-15 the gates of the same 8 outputs) instead of alternating 16-row
-// blocks, so a wave tile needs no value/gate block pairs: the 4x2 wave layout (fewer LDS fragment
-// reads per MFMA than 8x1) becomes possible; the epilogue pairs lanes l / l^32 by v_permlane32_swap
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0, bool GILV = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __restrict__ partial) {
   constexpr bool SPREAD = SCHED == 1;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -96,8 +95,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
   static_assert(CONV == 0 || CONV == 2, "buffer-resource A modes only");
   constexpr int TI = G::TI, TJ = G::TJ, TIa = G::TIa, TIb = G::TIb, TJa = G::TJa, TJb = G::TJb;
   static_assert(TIb >= 1 && TJb >= 1, "each wave tile splits into 2 x 2 quadrants");
-  static_assert(!GEGLU || GILV || (TI % 2 == 0), "geglu pairs");
-  static_assert(!GILV || GEGLU, "interleaved gates: gated tiles only");
+  static_assert(!GEGLU || (TI % 2 == 0), "geglu pairs");
   constexpr int TILE = G::TILE_ROWS * 8;   // uint4 per buffer
   constexpr int OOB = (int)0x80000000;
 
@@ -198,11 +196,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
     const int br = w_row(h, rho);   // block n row
     int gr = -1;
     if (rho < R && br < BN) {
-      if constexpr (GILV) {
-        const int blk = br >> 4, within = br & 15;
-        const int nout = n0 + blk * 8 + (within & 7);
-        gr = (nout < p.N) ? ((within & 8) ? p.N + nout : nout) : -1;
-      } else if constexpr (GEGLU) {
+      if constexpr (GEGLU) {
         const int blk = br >> 4, within = br & 15;
         const int nout = n0 + (blk >> 1) * 16 + within;
         gr = (nout < p.N) ? ((blk & 1) ? p.N + nout : nout) : -1;
@@ -537,11 +531,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
   wait_vmcnt<0>();
   __syncthreads();
 
-  tile_epilogue<BM, BN, WM, WN, GEGLU, false, TI, TJ, 512, true, GILV>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
+  tile_epilogue<BM, BN, WM, WN, GEGLU, false, TI, TJ, 512, true>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
                                                           gridDim.y, blockIdx.y);
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, bool GILV = false>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU>
 void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -550,7 +544,7 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   // the two-phase schedule (SCHED 2; 593 -> 573 ms/step, commit 88fbe5c).  SCHED 0 / 1 are no
   // longer instantiated in the library (tools/ppdiag.hip still builds them for diagnostics)
-  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, PP_DIAG_DEFAULT, GILV>;
+  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, PP_DIAG_DEFAULT>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -569,8 +563,6 @@ void launch_pp_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
     // (wave tile 32 x 160: 5 value/gate pairs), 80 outputs per block -- at M = 2048 x 5120 that
     // is 512 blocks = 2 full rounds instead of 640 = 2.5 rounds of the 64-output 256 x 128 tile
     if (p.cfg == 8) launch_pp<256, 160, 8, 1, CONV, true>(p, ws, s);
-    // cfg 23: the same 80-output tile on the 4x2 wave layout (wave tile 64 x 80) with interleaved gates
-    else if (p.cfg == 23) launch_pp<256, 160, 4, 2, CONV, true, true>(p, ws, s);
     else launch_pp<256, 128, 4, 2, CONV, true>(p, ws, s);
     return;
   }

@@ -253,13 +253,12 @@ def test_layer_norm_folded_into_gemm(rows, K, N, act, res):
     assert rel_err(out, exp) < 1.5e-2
 
 
-@pytest.mark.parametrize("cfg", [31, 33, 23, 8])
+@pytest.mark.parametrize("cfg", [31, 33, 8])
 def test_layer_norm_folded_into_producer_wave_gemm(cfg, force_cfg):
     """the level-3 projection / GEGLU shapes on the warp-specialised tiles (31, 33: 8 MFMA + 8
-    producer waves) and the gated ping-pong tiles (8: 8x1 waves, 23: 4x2 waves with interleaved
-    value / gate rows): folded LayerNorm epilogue (row statistics + wsum correction) and bias; a
-    gated call forced onto a deep-ring config takes the gated deep-ring tile (12), a plain call
-    forced onto 23 the ping-pong 256x256 tile"""
+    producer waves) and the gated ping-pong tile (8: 8x1 waves): folded LayerNorm epilogue (row
+    statistics + wsum correction) and bias; a gated call forced onto a deep-ring config takes the
+    gated deep-ring tile (12)"""
     rows, K, N = 2048, 1280, 1280
     x = rnd(rows, K, seed=76) * 1.5 + 0.3
     g = rnd(K, seed=77) * 0.3 + 1
@@ -528,7 +527,7 @@ def test_latent_step_matches_reference(sched):
 
 
 # ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
-PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 23, 26, 27, 31, 32, 33]   # ping-pong (7-10, 20-23), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-33)
+PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 26, 27, 31, 32, 33]   # ping-pong (7-10, 20-22), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-33)
 
 
 @pytest.fixture
