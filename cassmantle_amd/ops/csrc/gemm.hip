@@ -39,7 +39,6 @@ constexpr int BK = 64;
 //       (M = 8192 x N = 640: 256 tiles)
 //   21: ping-pong 128x128 (4x2 waves, wave 32x64, 64 KiB LDS: 2 blocks per CU)
 //   22: ping-pong 128x64 (4x2 waves, 48 KiB LDS)
-//   23 / 24: ping-pong 128x160 / 128x128 with 8 LDS-DMA-only producer waves (gemm_pp.h NPW)
 //   26 / 27: 8-wave 128x80 (8x1 waves, wave 16x80, 4-stage ring) / 128x64 (4x2 waves, 3 stages):
 //       the small-grid tiles with twice the waves issuing LDS-DMA.  A CU's LDS-DMA fill rate is
 //       set by the number of waves issuing it, not by the bytes in flight (4 waves: 22 B/cycle
@@ -53,17 +52,16 @@ constexpr int BK = 64;
 // profiles/r2_regstage_ab.txt), 23 (ping-pong 256x64), 24/25 (halo-staged 3x3 conv,
 // profiles/r3_bench_halo.jsonl), 28 (16-wave 128x64, profiles/r3_probe_16wave.jsonl), 29/30 (8-wave
 // 128x128 / 256x80 and the gated 128x128, profiles/r3_tune_8wave_b_ab.txt,
-// profiles/r3_tune_8wave_gated.txt).  Their indices stay reserved so table keys keep their meaning
-// (23 and 24 are reused by the producer-wave ping-pong tiles; no table entry referred to them).
+// profiles/r3_tune_8wave_gated.txt).  Their indices stay reserved so table keys keep their meaning.
 // Configs >= 11 are chosen only from the measured tuning table (gemm_tune_*) or when forced.
 struct TileCfg { int BM, BN; float eff; int slots; };
 constexpr int kNumTiles = 34;
 constexpr int kPP128 = 20, kPP128x128 = 21;
 // ping-pong configs outside the 7..10 block (dispatch and eligibility)
-constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || (c >= 20 && c <= 24); }
+constexpr bool is_pp_cfg(int c) { return (c >= 7 && c < 11) || c == 20 || c == 21 || c == 22; }
 // configs with a kernel behind them (the reserved indices above have none)
 constexpr bool is_live_cfg(int c) {
-  return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 24) || c == 26 || c == 27 ||
+  return (c >= 0 && c <= 10) || (c >= 12 && c <= 16) || (c >= 20 && c <= 22) || c == 26 || c == 27 ||
          (c >= 31 && c <= 33);
 }
 constexpr int kAreg = 15;
@@ -79,8 +77,8 @@ constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 1.00f, 512}, {128, 160, 1.02f,
                                        {128, 128, 1.f, 256},   {128, 64, 1.f, 256},    {128, 160, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 768},
                                        {128, 128, 1.f, 512},   {128, 160, 1.f, 512},   {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {128, 160, 1.f, 256},
-                                       {128, 128, 1.f, 256},   {128, 160, 1.f, 256},   {128, 80, 1.f, 256},
+                                       {128, 128, 1.f, 512},   {128, 64, 1.f, 768},    {256, 64, 1.f, 512},
+                                       {256, 160, 1.f, 256},   {128, 160, 1.f, 256},   {128, 80, 1.f, 256},
                                        {128, 64, 1.f, 256},    {128, 64, 1.f, 256},    {128, 128, 1.f, 256},
                                        {256, 80, 1.f, 256},    {128, 80, 1.f, 256},    {128, 64, 1.f, 256},
                                        {128, 160, 1.f, 256}};

@@ -83,15 +83,14 @@ CM_DEVICE bf16x8_t gn_silu_probe(bf16x8_t a, int lane) {
 // (A gated 256x160 tile on 4x2 waves -- value / gate rows interleaved at 8-row granularity, paired
 // by v_permlane32_swap in the epilogue -- was correct but no faster than the 8x1 gated tile on the
 // level-3 GEGLU, 68.3 us; round 4, profiles/r4_producer_waves_ab.txt.)
+// (8 LDS-DMA-only producer waves beside the 8 MFMA waves of the 128x160 / 128x128 tiles, issuing
+// the parts at the same barrier points, 1 block per CU: correct, picked for 9 shapes in situ, but
+// the bench step was 0.7 % slower; round 4, profiles/r4_producer_waves_ab.txt.)
 // DIAG (timing diagnostics only, tools/ppdiag.hip; results are wrong): bit 0 drops the mainloop
 // DMA, bit 1 its barriers, bit 2 adds a GroupNorm+SiLU cost probe on the A fragments (variant
 // builds with -DPP_DIAG_DEFAULT=4, profiles/r4_gn_prologue_probe.txt)
-// NPW = 8 (SCHED 2 only): 8 LDS-DMA-only producer waves beside the 8 ping-pong MFMA waves (1024
-// threads).  The producers issue every part at the same points of the barrier sequence as the MFMA
-// waves did (W of t+1 before the first barrier of k-tile t, A of t+2 after its second) and wait
-// for k-tile t+1 before its fourth, so the MFMA waves' load segments hold only fragment reads.
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0, int NPW = 0>
-__global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, float* __restrict__ partial) {
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int SCHED, int DIAG = 0>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __restrict__ partial) {
   constexpr bool SPREAD = SCHED == 1;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   using G = PPGeom<BM, BN, WM, WN>;
@@ -106,12 +105,8 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  static_assert(NPW == 0 || (NPW == 8 && SCHED == 2 && DIAG == 0), "producer waves: SCHED 2");
-  const bool prod = NPW > 0 && wave >= 8;  // DMA-only producer wave
-  const bool stager = NPW == 0 || prod;
-  const int swave = prod ? wave - 8 : wave;   // index among the staging waves
-  const int wm = wave % WM, wn = (prod ? 0 : wave) / WM;
-  const bool late = !prod && wave >= 4;    // staggered half (one barrier behind)
+  const int wm = wave % WM, wn = wave / WM;
+  const bool late = wave >= 4;             // staggered half (one barrier behind)
 
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -128,7 +123,7 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
   // ---- per-lane DMA state.  LDS region row rho of round r: 64 r + 8 wave + (lane >> 3); the
   // lane moves logical chunk (lane & 7) ^ swz of that row (source-side swizzle, rule 21).
   const int slot = lane & 7;
-  const int rsub = 8 * swave + (lane >> 3);
+  const int rsub = 8 * wave + (lane >> 3);
   auto chunk_of = [&](int ldsrow) { return slot ^ ((ldsrow >> 1) & 7); };
   // block row (0..BM) of A region h (0: m-half a, 1: m-half b), region row rho
   auto a_row = [&](int h, int rho) {
@@ -234,8 +229,8 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
 
   // ---- stage part PT of k-tile u into buffer b (every wave issues exactly NR_PT DMAs)
   auto dst = [&](int b, int regoff, int r, int R) -> uint4* {
-    const bool real = 64 * r + 8 * swave < R;   // wave-uniform
-    return real ? smem + b * TILE + (regoff + 64 * r + 8 * swave) * 8 : smem + (G::JUNK_ROW + 8 * swave) * 8;
+    const bool real = 64 * r + 8 * wave < R;   // wave-uniform
+    return real ? smem + b * TILE + (regoff + 64 * r + 8 * wave) * 8 : smem + (G::JUNK_ROW + 8 * wave) * 8;
   };
   auto stage = [&](auto PTc, int u, int b) {
     constexpr int PT = decltype(PTc)::value;
@@ -308,15 +303,13 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
 
   // ---- prologue: parts 0..5 (k-tile 0 whole, k-tile 1 A-a / W-a), then retire k-tile 0's
   // first two parts (PERIOD DMAs = one of each part type may stay in flight)
-  if (nk > 0 && stager) {
+  if (nk > 0) {
     stage(I0{}, kt0, 0);
     stage(I1{}, kt0, 0);
     stage(I2{}, kt0, 0);
     stage(I3{}, kt0, 0);
   }
-  if (!stager) {
-    // MFMA waves of a producer block: nothing in flight
-  } else if (nk > 1) {
+  if (nk > 1) {
     if constexpr (SCHED >= 2) {            // k-tile 1's A halves (issued by "P1 of k-tile -1")
       stage(I0{}, kt0 + 1, 1);
       stage(I2{}, kt0 + 1, 1);
@@ -458,9 +451,7 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
         for (int i = 0; i < TIb; ++i) wfb[i][ks] = as_bf16x8(Bs[wbase_b + 128 * i + lo[ks]]);
     }
     const int u = t + (P == 0 ? 1 : 2);
-    if constexpr (NPW > 0) {
-      // the producers stage; these waves only read fragments
-    } else if (!(DIAG & 1) && u < nk) {
+    if (!(DIAG & 1) && u < nk) {
       if constexpr (P == 0) {
         stage(I1{}, kt0 + u, B ^ 1);
         stage(I3{}, kt0 + u, B ^ 1);
@@ -518,27 +509,7 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
   };
 
   // two k-tiles per iteration so the buffer of every phase is a compile-time offset
-  if (prod) {
-    // producer schedule over the same barrier sequence: b1..b4 of k-tile t are the early half's
-    // X0 / Y0 / X1 / Y1 barriers (the late half runs one behind)
-    for (int t = 0; t < nk; ++t) {
-      const int b = t & 1;
-      if (t + 1 < nk) {                    // W of t+1 into the other buffer: its W rows were last
-        stage(I1{}, kt0 + t + 1, b ^ 1);   // read (k-tile t-1) before b4(t-1)
-        stage(I3{}, kt0 + t + 1, b ^ 1);
-      }
-      __builtin_amdgcn_s_barrier();        // b1(t)
-      __builtin_amdgcn_s_barrier();        // b2(t): both halves have read A of t
-      if (t + 2 < nk) {
-        stage(I0{}, kt0 + t + 2, b);
-        stage(I2{}, kt0 + t + 2, b);
-      }
-      __builtin_amdgcn_s_barrier();        // b3(t)
-      if (t + 2 < nk) wait_vmcnt<G::NR0 + G::NR2>();   // k-tile t+1 landed (only A of t+2 in flight)
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();        // b4(t): the early half reads k-tile t+1 after it
-    }
-  } else if constexpr (SCHED == 2) {
+  if constexpr (SCHED == 2) {
     for (int t = 0; t < nk; t += 2) {
       mphase(I0{}, I0{}, t);
       mphase(I1{}, I0{}, t);
@@ -563,11 +534,11 @@ __global__ void __launch_bounds__(512 + 64 * NPW, 1) gemm_pp_kernel(GemmArgs p, 
   wait_vmcnt<0>();
   __syncthreads();
 
-  tile_epilogue<BM, BN, WM, WN, GEGLU, false, TI, TJ, 512 + 64 * NPW, true>(p, acc, smem, partial, m0, n0, batch, wm, wn,
-                                                                         tid, gridDim.y, blockIdx.y, !prod);
+  tile_epilogue<BM, BN, WM, WN, GEGLU, false, TI, TJ, 512, true>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
+                                                          gridDim.y, blockIdx.y);
 }
 
-template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU, int NPW = 0>
+template <int BM, int BN, int WM, int WN, int CONV, bool GEGLU>
 void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
@@ -576,14 +547,14 @@ void launch_pp(const GemmArgs& p, float* ws, hipStream_t s) {
   constexpr size_t lds = pp_lds_bytes<BM, BN, WM, WN, GEGLU>();
   // the two-phase schedule (SCHED 2; 593 -> 573 ms/step, commit 88fbe5c).  SCHED 0 / 1 are no
   // longer instantiated in the library (tools/ppdiag.hip still builds them for diagnostics)
-  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, NPW ? 0 : PP_DIAG_DEFAULT, NPW>;
+  auto* kfn = &gemm_pp_kernel<BM, BN, WM, WN, CONV, GEGLU, 2, PP_DIAG_DEFAULT>;
   // > 64 KiB dynamic LDS opt-in, once per process (thread-safe static init)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL(kfn, grid, dim3(512 + 64 * NPW), lds, s, p, ws);
+  hipLaunchKernelGGL(kfn, grid, dim3(512), lds, s, p, ws);
   if (split > 1) launch_splitk_reduce<false>(p, ws, split, s);
 }
 
@@ -605,9 +576,6 @@ void launch_pp_cfg(const GemmArgs& p, float* ws, hipStream_t s) {
     case 20: launch_pp<128, 160, 4, 2, CONV, false>(p, ws, s); break;
     case 21: launch_pp<128, 128, 4, 2, CONV, false>(p, ws, s); break;
     case 22: launch_pp<128, 64, 4, 2, CONV, false>(p, ws, s); break;
-    // ping-pong 128x160 / 128x128 with 8 LDS-DMA-only producer waves (1024 threads, 1 block/CU)
-    case 23: launch_pp<128, 160, 4, 2, CONV, false, 8>(p, ws, s); break;
-    case 24: launch_pp<128, 128, 4, 2, CONV, false, 8>(p, ws, s); break;
     default: launch_pp<256, 256, 4, 2, CONV, false>(p, ws, s); break;
   }
 }

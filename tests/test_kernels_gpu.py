@@ -527,7 +527,7 @@ def test_latent_step_matches_reference(sched):
 
 
 # ---------------------------------------------------------------- ping-pong 8-wave GEMM (gemm_pp.h)
-PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 23, 24, 26, 27, 31, 32, 33]   # ping-pong (7-10, 20-22, producer-wave 23/24), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-33)
+PP_CFGS = [7, 8, 9, 10, 12, 13, 14, 16, 20, 21, 22, 26, 27, 31, 32, 33]   # ping-pong (7-10, 20-22), deep-ring (12-14, 16, 8-wave 26/27, producer-wave 31-33)
 
 
 @pytest.fixture
