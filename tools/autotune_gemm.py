@@ -28,7 +28,7 @@ from cassmantle_amd.ops._ext import ext  # noqa: E402
 
 # the live tile configs (gemm.hip is_live_cfg): 0-10 4/8-wave and ping-pong tiles, 12-14 deep ring,
 # 15 = A-in-registers short-K kernel, 16 = 128x80 deep ring, 20-22 = pp 128x160 / 128x128 / 128x64,
-# 26/27 = 8-wave 128x80 / 128x64 deep ring
+# 26/27 = 8-wave 128x80 / 128x64 deep ring, 31-33 = producer-wave 128x80 / 128x64 / 128x160 deep rings
 CFGS = [*range(0, 11), 12, 13, 14, 15, 16, 20, 21, 22, 26, 27, 31, 32, 33]
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
 
