@@ -590,10 +590,6 @@ static void launch_apply(const uint16_t* x, const uint16_t* x2, const long long*
     const long long per_img = (GN_APPLY_BLOCKS + B - 1) / B;
     const long long want = (S + per_img - 1) / per_img;
     rpb = step * ((want + step - 1) / step);
-    // very small tensors (the 8^2 x 2560 apply: 64 blocks of 8 rows): half-step blocks, as the
-    // round-3 sizing did (7.4 -> 6.9 us; with the round-3 threshold of 256 blocks the 16^2 x 1280
-    // apply, 176 blocks, lost 20 %: profiles/r4_gn_apply_variants.txt)
-    if (rpb == step && ((S + rpb - 1) / rpb) * B < 128) rpb = step / 2 >= g.R ? step / 2 : g.R;
   } else {
     long long want = 32;
     if (want < (32LL << 10) / (2LL * C)) want = (32LL << 10) / (2LL * C);
