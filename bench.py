@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--overlap", action="store_true", help="VAE decode on a side stream, overlapped with the next step's denoise")
     p.add_argument("--no-batch1", action="store_true", help="skip the batch-1 latency (s/image one room waits)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--oversubscribe", action="store_true",
+                   help="allow --gpus N above the visible GPU count: the N ranks share the GPUs "
+                        "(rank r on GPU r mod visible) over gloo with a host gather; RCCL refuses "
+                        "two ranks on one device, so nccl is refused here")
     return p.parse_args()
 
 
@@ -140,6 +144,8 @@ def launch_ranks(args) -> int:
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if args.oversubscribe:
+            env["CASSMANTLE_DIST_BACKEND"] = "gloo"
         # host threads per rank (torchrun's default is 1): N ranks must not each spin up a
         # thread per core of the machine
         env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
@@ -174,10 +180,17 @@ def main() -> int:
     if env_world is not None and int(env_world) != args.gpus:
         print(f"[bench] WORLD_SIZE={env_world} disagrees with --gpus {args.gpus}", file=sys.stderr)
         return 2
+    if args.oversubscribe:
+        if os.environ.get("CASSMANTLE_DIST_BACKEND", "gloo") != "gloo":
+            print("[bench] --oversubscribe runs gloo (RCCL refuses two ranks on one GPU); "
+                  f"CASSMANTLE_DIST_BACKEND={os.environ['CASSMANTLE_DIST_BACKEND']} refused", file=sys.stderr)
+            return 2
+        os.environ["CASSMANTLE_DIST_BACKEND"] = "gloo"
     if env_world is None and args.gpus > 1:
         n_vis = _visible_gpus()
-        if n_vis and args.gpus > n_vis:
-            print(f"[bench] --gpus {args.gpus} exceeds the {n_vis} visible GPU(s)", file=sys.stderr)
+        if n_vis and args.gpus > n_vis and not args.oversubscribe:
+            print(f"[bench] --gpus {args.gpus} exceeds the {n_vis} visible GPU(s) "
+                  "(--oversubscribe shares them over gloo)", file=sys.stderr)
             return 2
         return launch_ranks(args)
     if env_world is None and args.gpus < 1:
@@ -276,10 +289,15 @@ def main() -> int:
         torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     mine = elapsed
+    # finiteness of the final LATENTS of the last TIMED generation (the uint8 image is finite by
+    # construction); read before the batch-1 runs below replace it
+    finite = bool(sd.last_finite.item()) if sd.last_finite is not None else None
     TRACER.flush()
     stage_ms = {k: v["mean_ms"] for k, v in TRACER.snapshot().items()
                 if k in ("encode", "denoise", "decode")}
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    # per-rank scalars: host tensors over gloo (no GPU all_gather there), device tensors over RCCL
+    cdev = device if (world == 1 or dist.get_backend() != "gloo") else torch.device("cpu")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -287,7 +305,7 @@ def main() -> int:
     if world > 1:
         # per-rank step time and device time of its image gather (C2, RCCL over xGMI), to rank 0
         ag = [a.elapsed_time(b) for a, b in gather_ms[args.warmup:]] or [0.0]   # ms
-        mine_t = torch.tensor([mine / args.steps * 1e3, float(np.mean(ag)) * 1e3], dtype=torch.float64, device=device)
+        mine_t = torch.tensor([mine / args.steps * 1e3, float(np.mean(ag)) * 1e3], dtype=torch.float64, device=cdev)
         allv = [torch.zeros_like(mine_t) for _ in range(world)]
         dist.all_gather(allv, mine_t)
         per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "gather_us": round(float(v[1]), 1)}
@@ -304,8 +322,6 @@ def main() -> int:
             sd.generate(p1, negative, [8 + i], steps=args.denoise_steps, scheduler=args.scheduler)
             lat1.append(time.perf_counter() - t1)
         b1 = round(float(np.median(lat1)), 4)
-    # finiteness of the final LATENTS (the uint8 image is finite by construction)
-    finite = bool(sd.last_finite.item()) if sd.last_finite is not None else None
 
     score = {}
     if rank == 0 and not args.no_score:
@@ -344,7 +360,8 @@ def main() -> int:
         }
         if per_rank is not None:
             out["per_rank"] = per_rank
-            out["comm"] = {"backend": dist.get_backend(), "world_size": world}
+            out["comm"] = {"backend": dist.get_backend(), "world_size": world,
+                           "oversubscribed": bool(args.oversubscribe)}
         print(json.dumps(out), flush=True)
     cdist.shutdown()
     return 0

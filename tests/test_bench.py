@@ -31,7 +31,8 @@ def test_bench_gpus2_spawns_two_ranks():
     assert len(lines) == 1, r.stdout                 # rank 0 only
     out = lines[0]
     assert out["n_gpus"] == 2
-    assert out["comm"] == {"backend": "gloo", "world_size": 2}
+    assert out["comm"] == {"backend": "gloo", "world_size": 2, "oversubscribed": False}
+    assert out["finite"] in (True, None)
     assert [p["rank"] for p in out["per_rank"]] == [0, 1]
     assert out["config"]["global_batch"] == 8
     # whole-job aggregate: 2 ranks x 4 images x 1 step over the slowest rank's time
@@ -66,3 +67,14 @@ def test_bench_live_supervised_topology():
     assert out["topology"] == "supervised" and out["n_gpus"] == 2
     assert out["devices"] == ["cpu:0", "cpu:1"] and not out["retired"]
     assert out["rounds"] >= 1 and out["images_per_s"] > 0 and out["requests"] > 0
+
+
+def test_bench_oversubscribe_forces_gloo_and_refuses_nccl():
+    r = _run(["--gpus", "2", "--oversubscribe", "--model", "tiny", "--steps", "1", "--warmup", "0", "--no-score"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json_lines(r.stdout)[0]
+    assert out["comm"] == {"backend": "gloo", "world_size": 2, "oversubscribed": True}
+    assert len(out["per_rank"]) == 2
+    r = _run(["--gpus", "2", "--oversubscribe", "--model", "tiny", "--steps", "1", "--warmup", "0", "--no-score"],
+             env_extra={"CASSMANTLE_DIST_BACKEND": "nccl"}, timeout=120)
+    assert r.returncode == 2 and "refused" in r.stderr

@@ -233,3 +233,36 @@ def test_clip_text_matches_transformers():
     # SDXL conditions on the penultimate layer's hidden state (before the final LayerNorm)
     assert (pen - ref.hidden_states[-2]).abs().max().item() < 1e-4
 
+
+def test_openclip_bigg_matches_transformers_with_projection():
+    """SDXL's second text tower (OpenCLIP bigG: exact-erf GELU, penultimate hidden state, pooled
+    EOS row through ``text_projection``; ``models/text.py:90,119-143``) against
+    ``transformers.CLIPTextModelWithProjection`` -- the conditioning of the reference's SDXL-base
+    (``/root/reference/src/backend.py:24``).  The pooled ``text_embeds`` feed SDXL's add-embeds."""
+    transformers = pytest.importorskip("transformers")
+    from cassmantle_amd.models.text import CLIPTextConfig as OurClip
+    V = 500
+    hf_cfg = transformers.CLIPTextConfig(vocab_size=V, hidden_size=64, intermediate_size=160, num_hidden_layers=3,
+                                         num_attention_heads=4, max_position_embeddings=77, hidden_act="gelu",
+                                         layer_norm_eps=1e-5, attention_dropout=0.0, projection_dim=48,
+                                         bos_token_id=V - 2, eos_token_id=V - 1, pad_token_id=V - 1)
+    torch.manual_seed(0)
+    hf = transformers.CLIPTextModelWithProjection(hf_cfg).eval()
+    ours = CLIPTextEncoder(OurClip(vocab_size=V, max_positions=77, dim=64, layers=3, heads=4, mlp=160,
+                                   act="gelu", projection_dim=48), dtype=torch.float32).eval()
+    missing = load_state(ours, hf.state_dict(), "clip", strict=False)
+    assert not missing, missing
+    # real token layout: BOS, words, EOS, then EOS padding (SD pads with <|endoftext|>)
+    texts = ["a gothic style piece depicting the following: a silent lantern tower", "river"]
+    ids, _ = ours.tokenizer(texts, pad_to=77)
+    assert ours.tokenizer.eos == V - 1 and (ids == V - 1).any(1).all()
+    with torch.no_grad():
+        ref = hf(input_ids=ids, output_hidden_states=True)
+        pen, pooled = ours(ids, output_hidden=-2)
+    assert (pen - ref.hidden_states[-2]).abs().max().item() < 1e-4
+    assert pooled.shape == ref.text_embeds.shape
+    assert (pooled - ref.text_embeds).abs().max().item() < 1e-4
+    # the exporter is the inverse mapping for the projection too
+    sd = export_diffusers(ours, "clip")
+    assert torch.equal(sd["text_projection.weight"], hf.state_dict()["text_projection.weight"])
+

@@ -103,6 +103,32 @@ def test_sd15_unet_full_size_vs_fp32_reference():
     assert c >= 0.999, c
 
 
+def test_sd15_unet_bench_batch8_plans():
+    """The headline bench's UNet shape: batch 8 (4 images x CFG) at 64^2, i.e. the M = 32768 /
+    8192 / 2048 / 512 GEMM rows with the tuned split-K and producer-wave plans the bench runs.
+    Two rows against the fp32 CPU reference (cos >= 0.999); every row against batch-2 runs of the
+    same inputs (different plans: cos >= 0.9999)."""
+    from cassmantle_amd.models.unet import SD15_UNET, UNet
+    m = UNet(SD15_UNET, seed=0).cuda()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(8, 64, 64, 4, generator=g).to(torch.bfloat16)
+    t = torch.tensor([801.0] * 8)
+    ctx = (torch.randn(8, 77, 768, generator=g) * 0.5).to(torch.bfloat16)
+    with torch.no_grad():
+        out8 = m(x.cuda(), t.cuda(), ctx.cuda()).float().cpu()
+        assert torch.isfinite(out8).all()
+        out2 = torch.cat([m(x[i:i + 2].cuda(), t[i:i + 2].cuda(), ctx[i:i + 2].cuda()).float().cpu()
+                          for i in range(0, 8, 2)])
+        rows = [0, 5]
+        ref = _fp32_cpu_copy(m)(x[rows].float(), t[rows], ctx[rows].float())
+    for j, r in enumerate(rows):
+        c = cos(out8[r], ref[j])
+        assert c >= 0.999, (r, c)
+    for r in range(8):
+        c = cos(out8[r], out2[r])
+        assert c >= 0.9999, (r, c)
+
+
 def test_sd_vae_decoder_full_size_vs_fp32_reference():
     """the full SD VAE decoder (64^2 latent -> 512^2 image: 512-channel convs, the d=512
     mid-block attention, the parity upsampling convs) vs the fp32 reference"""
