@@ -84,6 +84,12 @@ class GameConfig:
     # src/backend.py:211-215) and the retired devices are re-probed after this long (doubling
     # per failed probe, capped at 1 h) instead of being lost for the life of the process
     device_reprobe_s: float = 120.0
+    # supervised groups: "async" hands each worker its rooms' next batch as soon as THAT worker
+    # is idle (a slow GPU holds only its own rooms); "lockstep" runs C1/C2/C4 collective rounds
+    supervisor_dispatch: str = "async"
+    # share of the rooms owned by the GPU the front-end's guess scorer also runs on (GPU 0);
+    # the other GPUs have weight 1 (parallel.rooms.RoomSharding)
+    frontend_device_weight: float = 0.85
     # --- multi-GPU guess scoring (parallel/scoring.py) ---
     score_topology: str = "central"       # central (rank 0 scores) | sharded (C1 broadcast + C3 gather)
     score_shard_min: int = 256            # sharded: smaller micro-batches are still scored on rank 0

@@ -675,9 +675,10 @@ def pair_cosine(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 def cosine_topk(table: torch.Tensor, vec: torch.Tensor, k: int):
     if not _use_hip(table):
         return ref.cosine_topk(table, vec, k)
-    s = torch.empty(table.shape[0], device=table.device, dtype=torch.float32)
-    ext().cosine_gemv(table, vec.contiguous(), s)
-    return torch.topk(s, k)
+    # one fused in-tree pipeline (misc.hip): block-wise cosine + bitonic top-k + merge passes;
+    # equal scores rank the lower row first (torch.return_types-like (values, indices))
+    vals, idx = ext().cosine_topk(table.contiguous(), vec.contiguous(), int(k))
+    return torch.return_types.topk((vals, idx))
 
 
 def mean_pool_l2(hidden: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:

@@ -543,6 +543,25 @@ void cosine_gemv(const at::Tensor& table, const at::Tensor& vec, at::Tensor& out
                      out.data_ptr<float>(), cur_stream());
 }
 
+// K15 most_similar: fused cosine GEMV + block top-k + merge passes (misc.hip), no ATen sort
+std::vector<at::Tensor> cosine_topk(const at::Tensor& table, const at::Tensor& vec, int64_t k) {
+  CHECK_DEV(table); CHECK_CONTIG(table); CHECK_CONTIG(vec);
+  TORCH_CHECK(table.dim() == 2 && vec.numel() == table.size(1), "cosine_topk: table [V, D], vec [D]");
+  TORCH_CHECK(table.size(0) < (1ll << 31), "cosine_topk: V must fit int32");
+  TORCH_CHECK(k >= 1 && k <= 1024 && k <= table.size(0), "cosine_topk: 1 <= k <= min(1024, V)");
+  int tf = table.scalar_type() == at::kFloat, vf = vec.scalar_type() == at::kFloat;
+  TORCH_CHECK(tf || table.scalar_type() == at::kBFloat16, "cosine_topk: table f32 or bf16");
+  TORCH_CHECK(vf || vec.scalar_type() == at::kBFloat16, "cosine_topk: vec f32 or bf16");
+  const int V = (int)table.size(0);
+  auto ws = at::empty({(int64_t)cosine_topk_workspace(V, (int)k)}, table.options().dtype(at::kLong));
+  auto vals = at::empty({k}, table.options().dtype(at::kFloat));
+  auto idx = at::empty({k}, table.options().dtype(at::kLong));
+  launch_cosine_topk(table.data_ptr(), tf, V, (int)table.size(1), vec.data_ptr(), vf, (int)k,
+                     reinterpret_cast<unsigned long long*>(ws.data_ptr<int64_t>()), vals.data_ptr<float>(),
+                     idx.data_ptr<int64_t>(), cur_stream());
+  return {vals, idx};
+}
+
 void mean_pool_l2(const at::Tensor& h, const at::Tensor& lens, at::Tensor& out) {
   CHECK_DEV(h); CHECK_BF16(h); CHECK_CONTIG(h);
   TORCH_CHECK(lens.scalar_type() == at::kInt, "lens must be int32");
@@ -819,6 +838,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gather_cosine", &gather_cosine, nogil());
   m.def("pair_cosine", &pair_cosine, nogil());
   m.def("cosine_gemv", &cosine_gemv, nogil());
+  m.def("cosine_topk", &cosine_topk, nogil());
   m.def("mean_pool_l2", &mean_pool_l2, nogil());
   m.def("gaussian_blur", &gaussian_blur, nogil());
   m.def("to_uint8", &to_uint8, nogil());

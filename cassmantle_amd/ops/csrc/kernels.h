@@ -172,6 +172,9 @@ void launch_gather_cosine(const void* table, int table_f32, int D, const int* ia
 void launch_pair_cosine(const float* a, const float* b, int D, float* out, int n, hipStream_t s);
 void launch_cosine_gemv(const void* table, int table_f32, int V, int D, const void* vec, int vec_f32,
                         float* out, hipStream_t s);
+int cosine_topk_workspace(int V, int k);
+void launch_cosine_topk(const void* table, int table_f32, int V, int D, const void* vec, int vec_f32, int k,
+                        unsigned long long* ws, float* vals, long long* idx, hipStream_t s);
 void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, int T, int D, hipStream_t s);
 
 // image / diffusion glue

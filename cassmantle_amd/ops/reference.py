@@ -177,7 +177,9 @@ def cosine_topk(table, vec, k):
     t = table.float()
     v = vec.float()
     s = (t @ v) / (t.norm(dim=-1) * v.norm()).clamp_min(1e-12)
-    return torch.topk(s, k)
+    # deterministic ties (the HIP kernel's contract): equal scores rank the lower row first
+    vals, idx = torch.sort(s, descending=True, stable=True)
+    return torch.return_types.topk((vals[:k], idx[:k]))
 
 
 def gaussian_kernel1d(sigma: float, device=None):

@@ -25,7 +25,21 @@ lock generates; a crashed holder's lock expires (120 s TTL) and any surviving wo
   restarts the group on the same devices (``max_restarts_without_culprit`` times);
 * with every device retired the rooms' rounds repeat (the reference's fallback), or a ``local``
   generator serves them, and the retired devices are re-probed with a fresh group after
-  ``reprobe_s`` (doubling per failed probe): a transient fault does not cost the GPUs forever.
+  ``reprobe_s`` (doubling per failed probe; reset only after the re-probed group served a round).
+  The probe starts the group on a background thread: requests arriving meanwhile fail fast
+  (their rooms repeat) instead of waiting for a group start.
+
+Two dispatch modes:
+
+* ``async`` (default): every worker has its own pipe; the front-end batches each worker's rooms
+  and hands a worker its next batch as soon as THAT worker is idle.  A slow GPU (GPU 0 shares its
+  device with the front-end's guess scorer) no longer holds the other GPUs' rooms at a round
+  barrier: a fast worker's rooms complete, and start their next round, first.  Rooms are sharded
+  by weight (``weights``: the scorer's device owns fewer rooms).  No collective runs after the
+  start handshake, so a dead worker cannot hang a peer inside RCCL.
+* ``lockstep``: the generation rounds of ``parallel.rooms.RankWorker`` -- C1 broadcast of the
+  job list from the leader, local generation, C2 device-resident RCCL gather to the leader, C4
+  barrier (the headline ``bench.py`` runs the same collectives).
 
 The legacy ``torchrun`` layout (front-end inside rank 0, ``serve.py`` under torchrun) is still
 supported; there a dead rank can only degrade the node to rank 0's GPU.
@@ -76,6 +90,8 @@ class WorkerSpec:
     slot: str = ""                  # the device label the front-end knows this worker by
     heartbeat_s: float = 0.5
     env: Dict[str, str] = field(default_factory=dict)
+    dispatch: str = "async"         # async | lockstep (module docstring)
+    weights: Optional[List[float]] = None
 
 
 def default_generator(cfg, device: str, spec: WorkerSpec) -> ImageGenerator:
@@ -98,7 +114,7 @@ def worker_main(spec: WorkerSpec, conn, hb, progress) -> None:
     import torch.distributed as dist
 
     from .dist import DistContext
-    from .rooms import STOP, RankWorker, RoomSharding
+    from .rooms import STOP, RankWorker, RoomSharding, generate_local
 
     stop_hb = threading.Event()
 
@@ -121,8 +137,23 @@ def worker_main(spec: WorkerSpec, conn, hb, progress) -> None:
 
         def done(rid: int) -> None:
             progress[spec.rank] = rid
-        worker = RankWorker(ctx, gen, RoomSharding(spec.room_ids, spec.world), spec.negative, on_local_done=done)
         dist.barrier()                                   # every member is up
+        if spec.dispatch == "async":
+            # the front-end drives this worker alone: no collective after the handshake
+            conn.send(("ready", os.getpid()))
+            while True:
+                msg = conn.recv()
+                if msg[0] == "stop":
+                    break
+                _, rid, jobs = msg
+                imgs = generate_local(gen, jobs, spec.negative)
+                done(rid)                                # device work finished (or failed)
+                conn.send(("result", rid, imgs, None))
+            dist.destroy_process_group()
+            stop_hb.set()
+            os._exit(0)
+        worker = RankWorker(ctx, gen, RoomSharding(spec.room_ids, spec.world, spec.weights), spec.negative,
+                            on_local_done=done)
         if spec.rank != 0:
             worker.serve_forever()
         else:
@@ -152,7 +183,8 @@ def worker_main(spec: WorkerSpec, conn, hb, progress) -> None:
 
 
 class _Group:
-    """One epoch of the worker group (front-end side handle)."""
+    """One epoch of the worker group (front-end side handle).  ``conns[r]`` is the pipe to
+    worker ``r`` (``async``: every worker; ``lockstep``: the leader only, ``conns[0]``)."""
 
     def __init__(self, devices: List[str], epoch: int, sup: "GroupSupervisor") -> None:
         self.devices = list(devices)
@@ -163,17 +195,32 @@ class _Group:
         self.progress = ctx.Array("i", W, lock=False)
         for r in range(W):
             self.progress[r] = -1
-        self.conn, child = ctx.Pipe()
+        per_worker = sup.dispatch == "async"
+        self.conns: List[Any] = []
+        children: List[Any] = []
+        for r in range(W if per_worker else 1):
+            a, b = ctx.Pipe()
+            self.conns.append(a)
+            children.append(b)
         port = free_port()
+        weights = sup.weights_for(devices)
         self.procs = []
         for r, d in enumerate(devices):
             spec = WorkerSpec(r, W, port, sup.device_name(d), sup.backend, sup.room_ids, sup.negative,
-                              sup.gen_factory, sup.cfg, epoch, d, sup.heartbeat_s, dict(sup.worker_env))
-            p = ctx.Process(target=worker_main, args=(spec, child if r == 0 else None, self.hb, self.progress),
+                              sup.gen_factory, sup.cfg, epoch, d, sup.heartbeat_s, dict(sup.worker_env),
+                              sup.dispatch, weights)
+            child = children[r] if per_worker else (children[0] if r == 0 else None)
+            p = ctx.Process(target=worker_main, args=(spec, child, self.hb, self.progress),
                             name=f"cassmantle-w{r}e{epoch}", daemon=True)
             p.start()
             self.procs.append(p)
+        for c in children:                   # the children hold their ends: EOF once they exit
+            c.close()
         self.started = time.time()
+
+    @property
+    def conn(self):
+        return self.conns[0]
 
     @property
     def world(self) -> int:
@@ -195,16 +242,18 @@ class _Group:
                     pass
         for p in self.procs:
             p.join(timeout=30)
-        try:
-            self.conn.close()
-        except Exception:  # noqa: BLE001
-            pass
+        for c in self.conns:
+            try:
+                c.close()
+            except Exception:  # noqa: BLE001
+                pass
 
     def stop(self, timeout: float = 30.0) -> None:
-        try:
-            self.conn.send(("stop",))
-        except Exception:  # noqa: BLE001
-            pass
+        for c in self.conns:
+            try:
+                c.send(("stop",))
+            except Exception:  # noqa: BLE001
+                pass
         t_end = time.time() + timeout
         for p in self.procs:
             p.join(timeout=max(0.1, t_end - time.time()))
@@ -212,15 +261,19 @@ class _Group:
 
 
 class GroupFailure(Exception):
-    def __init__(self, reason: str, culprits: Sequence[int]) -> None:
+    def __init__(self, reason: str, culprits: Sequence[int], group: Optional[_Group] = None) -> None:
         super().__init__(reason)
         self.culprits = list(culprits)
+        self.group = group
 
 
 class GroupSupervisor:
     """Front-end owner of the worker group.  ``submit(room, prompts, seeds)`` -> Future of the
-    room's images; rooms are sharded over the group's live workers (room ``i`` -> worker
-    ``i mod W``, ``parallel.rooms.RoomSharding``)."""
+    room's images; rooms are sharded over the group's live workers by weight
+    (``parallel.rooms.RoomSharding``; equal weights: room ``i`` -> worker ``i mod W``).
+
+    ``weights`` maps a device label to its share (default 1.0); ``dispatch`` is ``async`` or
+    ``lockstep`` (module docstring)."""
 
     def __init__(self, cfg, devices: Sequence[str], room_ids: Sequence[str], backend: Optional[str] = None,
                  gen_factory: str = "cassmantle_amd.parallel.supervisor:default_generator",
@@ -228,13 +281,26 @@ class GroupSupervisor:
                  heartbeat_s: float = 0.5, start_timeout_s: float = 900.0, watch_period_s: float = 0.2,
                  max_restarts_without_culprit: int = 2, local: Optional[ImageGenerator] = None,
                  worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None,
-                 reprobe_s: float = 120.0) -> None:
+                 reprobe_s: float = 120.0, dispatch: str = "async",
+                 weights: Optional[Dict[str, float]] = None) -> None:
+        if dispatch not in ("async", "lockstep"):
+            raise ValueError(f"dispatch must be async or lockstep, not {dispatch!r}")
         self.cfg = cfg
         self.all_devices = list(devices)
+        if len(set(self.all_devices)) != len(self.all_devices):
+            raise ValueError(f"duplicate device labels {self.all_devices} (use cuda:0#1 for a second slot)")
         self.healthy = list(devices)
         self.retired: Dict[str, str] = {}
         self.room_ids = list(room_ids)
-        self.backend = backend or ("nccl" if any(d.startswith("cuda") for d in devices) else "gloo")
+        self.dispatch = dispatch
+        self.weights = dict(weights or {})
+        shared = len({self.device_name(d) for d in devices}) < len(devices)
+        if backend is None:
+            # RCCL refuses two ranks on one device: slots that share a GPU run gloo
+            backend = "nccl" if any(d.startswith("cuda") for d in devices) and not shared else "gloo"
+        elif backend == "nccl" and shared:
+            raise ValueError("nccl (RCCL) cannot run two workers on one GPU; use gloo")
+        self.backend = backend
         self.gen_factory = gen_factory
         self.negative = cfg.game.negative_prompt
         self.window = window_s
@@ -249,16 +315,23 @@ class GroupSupervisor:
         self.resolution = resolution or cfg.model.resolution
         self.epoch = 0
         self.group: Optional[_Group] = None
+        self.sharding = None
         self.failures: List[Dict[str, Any]] = []
         self.rounds = 0
+        self.worker_rounds: Dict[str, int] = {}
         self.gather_us: List[float] = []
         self._blind = 0
         self._round_id = 0
         self.reprobe_s = reprobe_s
         self._probe_backoff = reprobe_s
         self._next_probe = float("inf")
+        self._probe_thread: Optional[threading.Thread] = None
+        self._probe_result: Optional[Tuple] = None
+        self._probation = False
         self.probes: List[Dict[str, Any]] = []
         self._q: "queue.Queue" = queue.Queue()
+        self._wake_r, self._wake_w = pymp.Pipe(duplex=False)
+        self._wake_lock = threading.Lock()
         self._closed = False
         self._ready = threading.Event()
         self._thread = threading.Thread(target=self._loop, name="group-supervisor", daemon=True)
@@ -267,27 +340,63 @@ class GroupSupervisor:
     # ------------------------------------------------------------------ devices / groups
     @staticmethod
     def device_name(d: str) -> str:
-        return "cpu" if d.startswith("cpu") else d      # "cpu:1" labels a CPU worker slot (tests)
+        """Device of a slot label: ``cpu:1`` labels a CPU worker slot (tests); ``cuda:0#1`` is a
+        second worker slot on ``cuda:0`` (one-GPU rehearsal of a multi-worker group, gloo)."""
+        return "cpu" if d.startswith("cpu") else d.split("#")[0]
+
+    def weights_for(self, devices: Sequence[str]) -> List[float]:
+        return [float(self.weights.get(d, self.weights.get(self.device_name(d), 1.0))) for d in devices]
+
+    def _spawn(self, devices: List[str]) -> _Group:
+        """Start a group on ``devices`` and wait for every pipe's ``ready``.  Raises GroupFailure
+        (carrying the group, so the caller kills it)."""
+        self.epoch += 1
+        g = _Group(devices, self.epoch, self)
+        t_end = time.time() + self.start_timeout
+        waiting = set(range(len(g.conns)))
+        while waiting:
+            for r in list(waiting):
+                c = g.conns[r]
+                try:
+                    if not c.poll(self.watch_period / max(1, len(waiting))):
+                        continue
+                    msg = c.recv()
+                except (EOFError, OSError) as e:        # the worker died before it reported
+                    f = self._diagnose(g, 0, f"worker pipe closed during start ({type(e).__name__})")
+                    f.group = g
+                    raise f
+                if msg[0] == "ready":
+                    waiting.discard(r)
+                    continue
+                f = self._diagnose(g, 0, f"worker start failed: {msg[-1].strip().splitlines()[-1][:300]}")
+                f.group = g
+                raise f
+            if not waiting:
+                break
+            if g.dead():
+                f = self._diagnose(g, 0, "worker exited during start")
+                f.group = g
+                raise f
+            if time.time() > t_end:
+                raise GroupFailure("worker group start timed out", [], g)
+        log.info("[INFO] worker group epoch %d up on %s (%s dispatch)", g.epoch, devices, self.dispatch)
+        return g
+
+    def _adopt(self, g: Optional[_Group]) -> None:
+        from .rooms import RoomSharding
+        self.group = g
+        self.sharding = RoomSharding(self.room_ids, g.world, self.weights_for(g.devices)) if g is not None else None
 
     def _start_group(self) -> None:
         if not self.healthy:
-            self.group = None
+            self._adopt(None)
             return
-        self.epoch += 1
-        g = _Group(self.healthy, self.epoch, self)
-        self.group = g
-        t_end = time.time() + self.start_timeout
-        while True:
-            if g.conn.poll(self.watch_period):
-                msg = g.conn.recv()
-                if msg[0] == "ready":
-                    log.info("[INFO] worker group epoch %d up on %s", self.epoch, self.healthy)
-                    return
-                raise self._diagnose(g, 0, f"worker start failed: {msg[-1].strip().splitlines()[-1][:300]}")
-            if g.dead():
-                raise self._diagnose(g, 0, "worker exited during start")
-            if time.time() > t_end:
-                raise GroupFailure("worker group start timed out", [])
+        try:
+            g = self._spawn(list(self.healthy))
+        except GroupFailure as e:
+            self.group = e.group                    # so _retire can name the culprits' devices
+            raise
+        self._adopt(g)
 
     def _retire(self, culprits: Sequence[int], reason: str) -> None:
         g = self.group
@@ -305,58 +414,116 @@ class GroupSupervisor:
                 for d in list(self.healthy):
                     self.retired[d] = "repeated group failures"
                 self.healthy.clear()
+        if self._probation:                           # a re-probed group failed before serving
+            self._probation = False
+            self._probe_backoff = min(2 * self._probe_backoff, 3600.0)
         if not self.healthy and self._next_probe == float("inf"):
             self._next_probe = time.time() + self._probe_backoff
         log.error("[ERROR] worker group epoch %d failed (%s); retired %s; healthy %s", self.epoch, reason, devs,
                   self.healthy)
 
-    def _restart(self, culprits: Sequence[int], reason: str) -> None:
-        self._retire(culprits, reason)
+    def _drop_group(self) -> None:
         if self.group is not None:
             self.group.kill()
-        self.group = None
+        self._adopt(None)
+
+    def _restart(self, culprits: Sequence[int], reason: str) -> None:
+        """Retire the culprits, kill the group, start a new one on the healthy devices.  Never
+        raises: every start failure (a worker that dies without reporting, an unexpected
+        message) retires what it can and tries the rest."""
+        self._retire(culprits, reason)
+        self._drop_group()
         while self.healthy and not self._closed:
             try:
                 self._start_group()
                 return
             except GroupFailure as e:
                 self._retire(e.culprits, str(e))
-                if self.group is not None:
-                    self.group.kill()
-                self.group = None
+            except Exception as e:  # noqa: BLE001 - never kill the supervisor thread
+                log.exception("[ERROR] worker group start failed unexpectedly")
+                self._retire([], f"start: {type(e).__name__}: {e}")
+            self._drop_group()
 
-    def _maybe_reprobe(self) -> None:
-        """With no live group: once the back-off has passed, put every retired device back and
-        try a fresh group on them (a failed probe retires them again and doubles the back-off)."""
-        if self.group is not None or not self.retired or self._closed or time.time() < self._next_probe:
-            return
+    # ------------------------------------------------------------------ re-probing (background)
+    def _probe_due(self) -> bool:
+        return (self.group is None and bool(self.retired) and not self._closed and self._probe_thread is None
+                and time.time() >= self._next_probe)
+
+    def _start_probe(self) -> None:
+        """With no live group and the back-off passed: start a fresh group on every retired
+        device on a background thread.  Requests keep failing fast meanwhile (a
+        probe must not hold a batch for a whole group start)."""
         back = [d for d in self.all_devices if d in self.retired]
         log.info("[INFO] re-probing retired devices %s", back)
-        t0 = time.time()
-        for d in back:
-            self.retired.pop(d, None)
-        self.healthy = [d for d in self.all_devices if d not in self.retired]
-        self._blind = 0
         self._next_probe = float("inf")
-        try:
-            self._start_group()
-        except GroupFailure as e:
-            self._restart(e.culprits, str(e))
-        ok = self.group is not None
-        self.probes.append({"devices": back, "ok": ok, "s": round(time.time() - t0, 3)})
-        if ok:
+        t0 = time.time()
+
+        def run():
+            try:
+                res = ("ok", self._spawn(back), back, t0)
+            except GroupFailure as e:
+                res = ("fail", e, back, t0)
+            except Exception as e:  # noqa: BLE001
+                res = ("fail", GroupFailure(f"probe: {type(e).__name__}: {e}", []), back, t0)
+            self._probe_result = res
+            self._wake()
+        self._probe_thread = threading.Thread(target=run, name="group-probe", daemon=True)
+        self._probe_thread.start()
+
+    def _finish_probe(self) -> None:
+        if self._probe_result is None:
+            return
+        self._probe_thread.join()
+        kind, obj, back, t0 = self._probe_result
+        self._probe_thread, self._probe_result = None, None
+        self.probes.append({"devices": back, "ok": kind == "ok", "s": round(time.time() - t0, 3)})
+        if kind == "ok":
+            if self._closed:
+                obj.kill()
+                return
+            for d in back:
+                self.retired.pop(d, None)
+            self.healthy = [d for d in self.all_devices if d not in self.retired]
+            self._blind = 0
+            self._probation = True                   # back-off resets after its first good round
+            self._adopt(obj)
+            return
+        if obj.group is not None:
+            obj.group.kill()
+        bad = [obj.group.devices[r] for r in obj.culprits if obj.group is not None and 0 <= r < obj.group.world]
+        self._probe_backoff = min(2 * self._probe_backoff, 3600.0)
+        self._next_probe = time.time() + self._probe_backoff
+        if bad and len(bad) < len(back):              # the innocent devices are tried again at once
+            for d in back:
+                if d not in bad:
+                    self.retired.pop(d, None)
+            self.healthy = [d for d in self.all_devices if d not in self.retired]
+            try:
+                self._start_group()
+            except GroupFailure as e:
+                self._restart(e.culprits, str(e))
+
+    def _round_ok(self) -> None:
+        self.rounds += 1
+        if self._probation:
+            self._probation = False
             self._probe_backoff = self.reprobe_s
-        else:
-            self._probe_backoff = min(2 * self._probe_backoff, 3600.0)
-            self._next_probe = time.time() + self._probe_backoff
 
     # ------------------------------------------------------------------ requests
+    def _wake(self) -> None:
+        with self._wake_lock:
+            try:
+                self._wake_w.send_bytes(b"w")
+            except Exception:  # noqa: BLE001
+                pass
+
     def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
         fut: cf.Future = cf.Future()
         if self._closed:
             fut.set_exception(ImageGenerationError("supervisor closed"))
             return fut
-        self._q.put((room, list(prompts), list(seeds), fut))
+        self._q.put((room, list(prompts), list(seeds), fut, time.monotonic()))
+        self._wake()
         return fut
 
     def wait_ready(self, timeout: Optional[float] = None) -> bool:
@@ -369,11 +536,13 @@ class GroupSupervisor:
     # peer) and reported it: collateral, not a culprit
     REPORTED_EXIT = 5
 
-    def _diagnose(self, g: "_Group", rid: int, reason: str, grace_s: float = 3.0) -> "GroupFailure":
+    def _diagnose(self, g: "_Group", rid: int, reason: str, grace_s: float = 3.0,
+                  suspects: Optional[Sequence[int]] = None) -> "GroupFailure":
         """Who broke the round.  A worker that died WITHOUT reporting (crash, OOM kill, signal)
         or stopped heart-beating is a culprit; peers whose collectives then failed exit with
         REPORTED_EXIT and are not.  With nobody dead, the workers that never finished their
-        local generation of round ``rid`` are (a wedged GPU: RCCL would block the rest)."""
+        local generation of round ``rid`` are (a wedged GPU: RCCL would block the rest);
+        ``suspects`` (async dispatch) names the workers whose own round timed out."""
         t_end = time.time() + grace_s
         while True:
             crashed = [r for r in g.dead() if g.procs[r].exitcode not in (0, self.REPORTED_EXIT)]
@@ -382,13 +551,16 @@ class GroupSupervisor:
                 break
             time.sleep(0.05)
         culprits = sorted(set(crashed) | set(stale))
-        if not culprits and rid > 0:
+        if not culprits and suspects is not None:
+            culprits = sorted(r for r in suspects if g.procs[r].exitcode is None)
+        elif not culprits and rid > 0:
             culprits = [r for r in range(g.world) if g.progress[r] < rid and g.procs[r].exitcode is None]
             if len(culprits) == g.world:         # nobody finished: no evidence against anyone
                 culprits = []
         codes = {r: g.procs[r].exitcode for r in range(g.world)}
         return GroupFailure(f"{reason}; exit codes {codes}", culprits)
 
+    # ------------------------------------------------------------------ lockstep rounds
     def _run_round(self, jobs) -> Dict[Tuple[str, int], np.ndarray]:
         g = self.group
         self._round_id += 1
@@ -412,48 +584,65 @@ class GroupSupervisor:
             if self.round_timeout > 0 and time.monotonic() - t0 > self.round_timeout:
                 raise self._diagnose(g, rid, f"round {rid} exceeded {self.round_timeout:.0f} s", grace_s=0.0)
 
-    def _loop(self) -> None:
-        from .rooms import GenJob
-        try:
-            self._start_group()
-        except GroupFailure as e:
-            self._restart(e.culprits, str(e))
-        self._ready.set()
+    def _next_batch(self) -> Optional[list]:
+        """Lockstep: block for a request, then collect more until every room is in or the
+        window closes.  None once closed."""
         while True:
-            item = self._q.get()
-            if item is None:
+            timeout = None
+            if self.group is None and (self._probe_thread is not None or self.retired):
+                timeout = self.watch_period
+            try:
+                item = self._q.get(timeout=timeout)
+            except queue.Empty:
+                self._tick_probe()
+                continue
+            break
+        if item is None:
+            return None
+        batch = [item]
+        t_end = time.monotonic() + self.window
+        every_room = set(self.room_ids)
+        while True:
+            # a room submits one request per round: once every room is in, the window closes
+            if every_room and {b[0] for b in batch} >= every_room:
                 break
-            batch = [item]
-            t_end = time.monotonic() + self.window
-            every_room = set(self.room_ids)
-            while True:
-                # a room submits one request per round: once every room is in, the window closes
-                if every_room and {b[0] for b in batch} >= every_room:
-                    break
-                rem = t_end - time.monotonic()
-                if rem <= 0:
-                    break
-                try:
-                    nxt = self._q.get(timeout=rem)
-                except queue.Empty:
-                    break
-                if nxt is None:
-                    self._q.put(None)
-                    break
-                batch.append(nxt)
-            if self.group is None:
-                self._maybe_reprobe()
+            rem = t_end - time.monotonic()
+            if rem <= 0:
+                break
+            try:
+                nxt = self._q.get(timeout=rem)
+            except queue.Empty:
+                break
+            if nxt is None:
+                self._q.put(None)
+                break
+            batch.append(nxt)
+        return batch
+
+    def _tick_probe(self) -> None:
+        self._finish_probe()
+        if self._probe_due():
+            self._start_probe()
+
+    def _loop_lockstep(self) -> None:
+        from .rooms import GenJob
+        while True:
+            batch = self._next_batch()
+            if batch is None:
+                break
+            self._tick_probe()
             if self.group is None:
                 self._serve_without_group(batch)
+                self._tick_probe()
                 continue
             jobs, spans = [], []
-            for room, prompts, seeds, fut in batch:
+            for room, prompts, seeds, fut, _ in batch:
                 s = len(jobs)
                 jobs.extend(GenJob(room, p, sd) for p, sd in zip(prompts, seeds))
                 spans.append((s, len(jobs), room, fut))
             try:
                 res = self._run_round(jobs)
-                self.rounds += 1
+                self._round_ok()
                 for s, e, room, fut in spans:
                     imgs = [res.get((room, i)) for i in range(s, e)]
                     if any(im is None for im in imgs):
@@ -463,25 +652,168 @@ class GroupSupervisor:
             except (GroupFailure, EOFError, OSError, BrokenPipeError) as e:
                 if not isinstance(e, GroupFailure):       # the leader's pipe broke
                     e = self._diagnose(self.group, self._round_id, f"leader pipe: {type(e).__name__}")
-                culprits = e.culprits
                 for *_, fut in spans:
                     if not fut.done():
                         fut.set_exception(ImageGenerationError(f"generation round failed: {e}"))
-                self._restart(culprits, str(e))
+                self._restart(e.culprits, str(e))
             except Exception as e:  # noqa: BLE001 - unexpected (message shape, pickling): never kill this thread
                 log.exception("[ERROR] supervisor round failed unexpectedly")
                 for *_, fut in spans:
                     if not fut.done():
                         fut.set_exception(ImageGenerationError(f"generation round failed: {type(e).__name__}: {e}"))
                 self._restart([], f"unexpected {type(e).__name__}: {e}")
-        if self.group is not None:
-            self.group.stop()
-            self.group = None
+
+    # ------------------------------------------------------------------ async (per-worker) rounds
+    def _loop_async(self) -> None:
+        """Each worker runs its own rounds: a worker is handed the pending requests of the rooms
+        it owns as soon as it is idle and either every one of its rooms has asked or the oldest
+        request waited ``window_s``.  Results resolve their rooms' futures as each worker
+        finishes; nothing waits for the slowest GPU."""
+        from multiprocessing.connection import wait as mp_wait
+        from .rooms import GenJob
+        pending: List[tuple] = []                 # (room, prompts, seeds, fut, t_submit)
+        busy: Dict[int, tuple] = {}               # worker -> (rid, spans, t0, n_jobs)
+        closing = False
+        while True:
+            # ---- collect requests
+            while True:
+                try:
+                    item = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if item is None:
+                    closing = True
+                    break
+                pending.append(item)
+            if closing:
+                break
+            self._tick_probe()
+            g = self.group
+            if g is None:
+                if pending:
+                    self._serve_without_group(pending)
+                    pending = []
+            else:
+                # ---- dispatch to idle workers
+                now = time.monotonic()
+                by_w: Dict[int, List[tuple]] = {}
+                for it in pending:
+                    by_w.setdefault(self.sharding.owner(it[0]), []).append(it)
+                for w, items in by_w.items():
+                    if w in busy:
+                        continue
+                    mine = set(self.sharding.rooms_of(w))
+                    if not ({it[0] for it in items} >= mine or now - min(it[4] for it in items) >= self.window):
+                        continue
+                    jobs, spans = [], []
+                    for room, prompts, seeds, fut, _ in items:
+                        s0 = len(jobs)
+                        jobs.extend(GenJob(room, p, sd) for p, sd in zip(prompts, seeds))
+                        spans.append((s0, len(jobs), room, fut))
+                    self._round_id += 1
+                    try:
+                        g.conns[w].send(("round", self._round_id, jobs))
+                    except (OSError, EOFError, BrokenPipeError):
+                        pass                              # detected below as a dead worker
+                    busy[w] = (self._round_id, spans, time.monotonic(), len(jobs))
+                    taken = set(map(id, items))
+                    pending = [it for it in pending if id(it) not in taken]
+            # ---- wait for results / requests / timers
+            timeout = self.watch_period if (busy or self._probe_thread is not None
+                                            or (self.group is None and self.retired)) else None
+            idle_waiting = [it[4] for it in pending if g is not None and self.sharding.owner(it[0]) not in busy]
+            if idle_waiting:                      # an idle worker's batching window closes
+                timeout = max(0.0, min(timeout if timeout is not None else 1e9,
+                                       min(idle_waiting) + self.window - time.monotonic()))
+            waitables = [self._wake_r] + [g.conns[w] for w in busy] if g is not None else [self._wake_r]
+            ready = mp_wait(waitables, timeout)
+            if self._wake_r in ready:
+                while self._wake_r.poll():
+                    self._wake_r.recv_bytes()
+            if g is None or not busy:
+                continue
+            # ---- results and failures
+            failure: Optional[GroupFailure] = None
+            for w in list(busy):
+                rid, spans, t0, n = busy[w]
+                c = g.conns[w]
+                if c in ready:
+                    try:
+                        msg = c.recv()
+                    except (EOFError, OSError) as e:
+                        failure = self._diagnose(g, rid, f"worker {w} pipe: {type(e).__name__}", suspects=[w])
+                        break
+                    if msg[0] == "result" and msg[1] == rid:
+                        del busy[w]
+                        imgs = msg[2]
+                        self._round_ok()
+                        dev = g.devices[w]
+                        self.worker_rounds[dev] = self.worker_rounds.get(dev, 0) + 1
+                        for s0, e0, room, fut in spans:
+                            got = imgs[s0:e0]
+                            if fut.done():
+                                continue
+                            if len(got) != e0 - s0 or any(im is None for im in got):
+                                fut.set_exception(ImageGenerationError(f"room {room}: generation failed"))
+                            else:
+                                fut.set_result(list(got))
+                        continue
+                    if msg[0] == "error":
+                        failure = self._diagnose(g, rid, f"worker {w} failed: "
+                                                 f"{msg[-1].strip().splitlines()[-1][:300]}", suspects=[w])
+                        break
+                if self.round_timeout > 0 and time.monotonic() - t0 > self.round_timeout:
+                    failure = self._diagnose(g, rid, f"worker {w} round {rid} exceeded {self.round_timeout:.0f} s",
+                                             grace_s=0.0, suspects=[w])
+                    break
+            if failure is None and busy:
+                if g.dead():
+                    failure = self._diagnose(g, max(b[0] for b in busy.values()), "worker exited",
+                                             suspects=[w for w in busy if g.procs[w].exitcode is not None])
+                elif g.stale(self.stale_s):
+                    failure = self._diagnose(g, 0, "worker stopped heart-beating", grace_s=0.0, suspects=[])
+            if failure is not None:
+                for _, spans, _, _ in busy.values():
+                    for *_, fut in spans:
+                        if not fut.done():
+                            fut.set_exception(ImageGenerationError(f"generation round failed: {failure}"))
+                busy.clear()
+                self._restart(failure.culprits, str(failure))
+        for it in pending:
+            if not it[3].done():
+                it[3].set_exception(ImageGenerationError("supervisor closed"))
+        for _, spans, _, _ in busy.values():
+            for *_, fut in spans:
+                if not fut.done():
+                    fut.set_exception(ImageGenerationError("supervisor closed"))
+
+    def _loop(self) -> None:
+        try:
+            self._start_group()
+        except GroupFailure as e:
+            self._restart(e.culprits, str(e))
+        except Exception as e:  # noqa: BLE001
+            log.exception("[ERROR] worker group start failed unexpectedly")
+            self._restart([], f"start: {type(e).__name__}: {e}")
+        self._ready.set()
+        try:
+            if self.dispatch == "async":
+                self._loop_async()
+            else:
+                self._loop_lockstep()
+        finally:
+            if self.group is not None:
+                self.group.stop()
+                self._adopt(None)
+            if self._probe_thread is not None:
+                self._probe_thread.join(timeout=self.start_timeout)
+                if self._probe_result is not None and self._probe_result[0] == "ok":
+                    self._probe_result[1].kill()
 
     def _serve_without_group(self, batch) -> None:
         """No live group: a ``local`` generator serves the batch, otherwise each room's round
         repeats (its request fails fast; the room keeps its content, src/backend.py:211-215)."""
-        for room, prompts, seeds, fut in batch:
+        for room, prompts, seeds, fut, *_ in batch:
             if self.local is None:
                 fut.set_exception(ImageGenerationError("no healthy generation device left: the round repeats"))
                 continue
@@ -495,14 +827,18 @@ class GroupSupervisor:
             return
         self._closed = True
         self._q.put(None)
+        self._wake()
         self._thread.join(timeout=120)
         if self.group is not None:
             self.group.kill()
-            self.group = None
+            self._adopt(None)
 
     def status(self) -> Dict[str, Any]:
         return {"epoch": self.epoch, "live_devices": self.live_devices(), "retired": dict(self.retired),
                 "rounds": self.rounds, "failures": list(self.failures), "probes": list(self.probes),
+                "dispatch": self.dispatch, "worker_rounds": dict(self.worker_rounds),
+                "owners": ({r: self.group.devices[self.sharding.owner(r)] for r in self.room_ids}
+                           if self.group is not None else {}),
                 "gather_us_p50": float(np.median(self.gather_us)) if self.gather_us else None}
 
 

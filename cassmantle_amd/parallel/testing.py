@@ -8,7 +8,9 @@ configured through the worker environment:
   crash), ``hang`` (the generation never returns but the process keeps heart-beating, like a
   wedged GPU kernel), ``fail`` (the generation raises), ``async_hang`` (``generate_device``
   returns at once, as the real pipeline does when it only QUEUES the work, but its completion
-  event never fires: a GPU wedged inside the denoise graph);
+  event never fires: a GPU wedged inside the denoise graph), ``slow`` (every generation takes
+  ``CASSMANTLE_FAULT_DELAY`` seconds longer: a straggler GPU), ``start_kill`` (the worker dies
+  while its generator is being built: a fault during model load or graph capture);
 * ``CASSMANTLE_FAULT_TRIGGER``: a file; the fault fires only once it exists.
 
 Every image carries the generating slot's index in its top-left 8x8 block (value
@@ -42,6 +44,8 @@ class StampedGenerator(SolidImageGenerator):
                 time.sleep(3600)
             if self.fault_mode == "fail":
                 raise ImageGenerationError("injected failure")
+            if self.fault_mode == "slow":
+                time.sleep(float(os.environ.get("CASSMANTLE_FAULT_DELAY", "1.0")))
         out = super().generate(prompts, negative_prompt, seeds)
         for im in out:
             im[:8, :8, :] = 40 * (self.index + 1)
@@ -76,6 +80,10 @@ class AsyncStampedGenerator(StampedGenerator):
 
 
 def stamped_generator(cfg, device: str, spec) -> StampedGenerator:
+    trig = os.environ.get("CASSMANTLE_FAULT_TRIGGER")
+    if (os.environ.get("CASSMANTLE_FAULT") == "start_kill" and (spec.slot or device) == os.environ.get("CASSMANTLE_FAULT_SLOT")
+            and trig and os.path.exists(trig)):
+        os._exit(17)                     # dies without reporting, before the "ready" message
     cls = AsyncStampedGenerator if os.environ.get("CASSMANTLE_FAULT") == "async_hang" else StampedGenerator
     return cls(spec.slot or device, res=cfg.model.resolution)
 

@@ -135,7 +135,8 @@ def _serve_supervised(cfg, args) -> int:
     # until a re-probe brings devices back (cfg.game.device_reprobe_s)
     sup = GroupSupervisor(cfg, devices, room_ids, round_timeout_s=cfg.game.round_timeout_s,
                           stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s,
-                          reprobe_s=cfg.game.device_reprobe_s)
+                          reprobe_s=cfg.game.device_reprobe_s, dispatch=cfg.game.supervisor_dispatch,
+                          weights={devices[0]: cfg.game.frontend_device_weight})
     sup.wait_ready()
     if cfg.model.scorer_stream_priority is None:
         cfg.model.scorer_stream_priority = 0      # no generation in this process (config.py)

@@ -207,7 +207,11 @@ def test_group_norm_statistics_of_a_concatenation():
 
 
 @pytest.mark.parametrize("B,H,Ca,Cb,N", [(8, 16, 1280, 640, 640), (2, 32, 640, 320, 320), (3, 8, 64, 192, 96),
-                                         (2, 5, 320, 320, 320)])
+                                         (2, 5, 320, 320, 320),
+                                         # the SD up-block 8x8 concatenation 1280|1280 (the two vectors
+                                         # of a thread come from different tensors), and a short last
+                                         # block (clamped-row loads) at that width
+                                         (8, 8, 1280, 1280, 1280), (3, 5, 1280, 1280, 1280)])
 def test_concat_free_gemm_and_group_norm(B, H, Ca, Cb, N):
     """UNet up-block [h | skip] consumers read the two tensors directly: the 1x1 shortcut GEMM
     stages k-tiles from both, the GroupNorm normalises both into one output."""
@@ -986,3 +990,37 @@ def test_gn_linear_folds_groupnorm_into_areg(B, S, C, N):
     assert tuple(ext().gemm_last_plan())[0] == 15
     exp = ref.linear(ref.group_norm(x.float(), 32, g.float(), be.float(), 1e-6, False).to(torch.bfloat16), w, b)
     assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("V,D,k,dtype", [(1, 300, 1, torch.float32), (5000, 300, 51, torch.bfloat16),
+                                         (100_003, 300, 64, torch.float32), (1_000_000, 300, 51, torch.bfloat16),
+                                         (70_000, 64, 1024, torch.bfloat16)])
+def test_cosine_topk_in_tree(V, D, k, dtype):
+    """K15 (``most_similar``, reference src/backend.py:297-301): fused cosine GEMV + bitonic
+    top-k + merge passes, no ATen kernel.  Exact ties (duplicated rows) rank the lower row
+    first, as the reference oracle's stable sort does."""
+    g = torch.Generator(device=DEV).manual_seed(V)
+    t = torch.randn(V, D, device=DEV, generator=g).to(dtype)
+    q = min(V - 1, 7)
+    if V > 100:                       # exact ties at the top: copies of the query row and of row 11
+        for j in (V // 3, V // 2, V - 1):
+            t[j] = t[q]
+        for j in (V // 5, V - 2):
+            t[j] = t[11]
+    vec = t[q]
+    v, i = ops.cosine_topk(t, vec, k)
+    ve, ie = ref.cosine_topk(t, vec, k)
+    assert v.dtype == torch.float32 and i.dtype == torch.int64 and v.shape == (k,) and i.shape == (k,)
+    assert torch.allclose(v, ve, atol=2e-5), (v[:8], ve[:8])
+    assert bool((v[:-1] >= v[1:]).all())                     # sorted, best first
+    # the same rows, up to rounding-level near-ties of the two reductions
+    same = i == ie
+    if not bool(same.all()):
+        bad = (~same).nonzero().flatten()
+        assert torch.allclose(v[bad], ve[bad], atol=2e-5)
+        assert set(i.tolist()) ^ set(ie.tolist()) <= set(i[bad].tolist()) | set(ie[bad].tolist())
+    if V > 100:
+        # exact ties (bit-identical rows): ascending row order inside each tie group
+        top = [q, V // 3, V // 2, V - 1]
+        assert i[:4].tolist() == sorted(top), i[:8]
+        assert torch.equal(v[:4], v[:1].expand(4))

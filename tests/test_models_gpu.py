@@ -106,8 +106,9 @@ def test_sd15_unet_full_size_vs_fp32_reference():
 def test_sd15_unet_bench_batch8_plans():
     """The headline bench's UNet shape: batch 8 (4 images x CFG) at 64^2, i.e. the M = 32768 /
     8192 / 2048 / 512 GEMM rows with the tuned split-K and producer-wave plans the bench runs.
-    Two rows against the fp32 CPU reference (cos >= 0.999); every row against batch-2 runs of the
-    same inputs (different plans: cos >= 0.9999)."""
+    Every row against the fp32 CPU reference (cos >= 0.999), and against batch-2 runs of the same
+    inputs, which take other plans: the two agree to cos >= 0.9998 (bf16 rounding of different
+    reduction orders) and the batch-8 rows are no further from fp32 than the batch-2 rows."""
     from cassmantle_amd.models.unet import SD15_UNET, UNet
     m = UNet(SD15_UNET, seed=0).cuda()
     g = torch.Generator().manual_seed(11)
@@ -119,14 +120,15 @@ def test_sd15_unet_bench_batch8_plans():
         assert torch.isfinite(out8).all()
         out2 = torch.cat([m(x[i:i + 2].cuda(), t[i:i + 2].cuda(), ctx[i:i + 2].cuda()).float().cpu()
                           for i in range(0, 8, 2)])
-        rows = [0, 5]
-        ref = _fp32_cpu_copy(m)(x[rows].float(), t[rows], ctx[rows].float())
-    for j, r in enumerate(rows):
-        c = cos(out8[r], ref[j])
-        assert c >= 0.999, (r, c)
-    for r in range(8):
-        c = cos(out8[r], out2[r])
-        assert c >= 0.9999, (r, c)
+        cpu = _fp32_cpu_copy(m)
+        ref = torch.cat([cpu(x[i:i + 2].float(), t[i:i + 2], ctx[i:i + 2].float()) for i in range(0, 8, 2)])
+    c8 = [cos(out8[r], ref[r]) for r in range(8)]
+    c2 = [cos(out2[r], ref[r]) for r in range(8)]
+    c82 = [cos(out8[r], out2[r]) for r in range(8)]
+    print("cos(b8, fp32)", c8, "cos(b2, fp32)", c2, "cos(b8, b2)", c82)
+    assert min(c8) >= 0.999, c8
+    assert min(c82) >= 0.9998, c82
+    assert min(a - b for a, b in zip(c8, c2)) >= -1e-4, (c8, c2)
 
 
 def test_sd_vae_decoder_full_size_vs_fp32_reference():

@@ -50,7 +50,7 @@ def test_supervised_group_on_cuda0():
     cfg.model.resolution = 16
     cfg.model.steps = 4
     rooms = ["", "1"]
-    sup = GroupSupervisor(cfg, ["cuda:0"], rooms, window_s=0.1, start_timeout_s=300)
+    sup = GroupSupervisor(cfg, ["cuda:0"], rooms, window_s=0.1, start_timeout_s=300, dispatch="lockstep")
     try:
         assert sup.backend == "nccl"
         assert sup.wait_ready(300) and sup.live_devices() == ["cuda:0"]
@@ -62,3 +62,34 @@ def test_supervised_group_on_cuda0():
     assert len(a) == 1 and len(b) == 2
     assert all(im.shape == (16, 16, 3) and im.dtype == np.uint8 for im in a + b)
     assert st["rounds"] >= 1 and not st["retired"] and st["gather_us_p50"] is not None, st
+
+
+@pytest.mark.parametrize("dispatch", ["async", "lockstep"])
+def test_supervised_two_slots_on_cuda0_gloo(dispatch):
+    """verdict r4 item 3: a 2-worker supervised group on ONE GPU (slots ``cuda:0`` and
+    ``cuda:0#1``; RCCL refuses two ranks on a device, so the group runs gloo): both workers draw
+    their own rooms, per-worker (async) or in C1/C2/C4 collective rounds (lockstep)."""
+    from cassmantle_amd.config import Config
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    cfg = Config()
+    cfg.model.image_model = "tiny"
+    cfg.model.resolution = 16
+    cfg.model.steps = 4
+    rooms = ["", "1", "2"]
+    sup = GroupSupervisor(cfg, ["cuda:0", "cuda:0#1"], rooms, window_s=0.1, start_timeout_s=300, dispatch=dispatch)
+    try:
+        assert sup.backend == "gloo"
+        assert sup.wait_ready(300) and sup.live_devices() == ["cuda:0", "cuda:0#1"]
+        owners = sup.status()["owners"]
+        assert owners == {"": "cuda:0", "1": "cuda:0#1", "2": "cuda:0"}, owners
+        futs = [sup.submit(r, [f"a castle {r}", "a river"], [1, 2]) for r in rooms]
+        imgs = [f.result(timeout=300) for f in futs]
+        st = sup.status()
+    finally:
+        sup.close()
+    assert all(len(x) == 2 and all(im.shape == (16, 16, 3) and im.dtype == np.uint8 for im in x) for x in imgs)
+    if dispatch == "async":
+        assert st["worker_rounds"].get("cuda:0", 0) >= 1 and st["worker_rounds"].get("cuda:0#1", 0) >= 1, st
+    else:
+        assert st["rounds"] >= 1 and st["gather_us_p50"] is None, st     # host (gloo) gather
+    assert not st["retired"], st

@@ -36,8 +36,9 @@ def _cfg(rooms):
     return cfg
 
 
-@pytest.mark.parametrize("fault", ["kill", "hang", "async_hang"])
-def test_dead_worker_retired_survivors_take_over(fault):
+@pytest.mark.parametrize("fault,dispatch", [("kill", "async"), ("hang", "async"), ("async_hang", "async"),
+                                            ("kill", "lockstep"), ("async_hang", "lockstep")])
+def test_dead_worker_retired_survivors_take_over(fault, dispatch):
     from fastapi.testclient import TestClient
     from cassmantle_amd.api.app import create_app
     from cassmantle_amd.game.imaging import decode_jpeg
@@ -49,7 +50,7 @@ def test_dead_worker_retired_survivors_take_over(fault):
         env = {"CASSMANTLE_FAULT_SLOT": "cpu:1", "CASSMANTLE_FAULT": fault, "CASSMANTLE_FAULT_TRIGGER": trig}
         sup = GroupSupervisor(_cfg(rooms), slots, rooms, gen_factory="cassmantle_amd.parallel.testing:stamped_generator",
                               window_s=0.3, round_timeout_s=8.0, stale_s=10.0, worker_env=env,
-                              start_timeout_s=240)
+                              start_timeout_s=240, dispatch=dispatch)
         try:
             assert sup.wait_ready(240)
             svc = _service(sup, rooms)
@@ -147,11 +148,109 @@ def test_every_device_lost_rounds_repeat_then_reprobe():
             with pytest.raises(ImageGenerationError, match="repeats"):
                 sup.submit("1", ["p"], [2]).result(timeout=30)
             assert time.time() - t0 < 5                       # fails fast: no group, no wait
-            time.sleep(2.5)
-            img = sup.submit("1", ["p"], [3]).result(timeout=240)
+            # the re-probe runs in the background once the back-off passed; requests keep failing
+            # fast meanwhile, the first one after the probe is served by the fresh group
+            img, t_end = None, time.time() + 240
+            while img is None and time.time() < t_end:
+                try:
+                    img = sup.submit("1", ["p"], [3]).result(timeout=30)
+                except ImageGenerationError as e:
+                    assert "repeats" in str(e)
+                    time.sleep(0.2)
             st = sup.status()
         finally:
             sup.close()
     assert slot_of(img[0]) == 0
     assert st["epoch"] == 2 and st["live_devices"] == ["cpu:0"] and not st["retired"], st
     assert [p["ok"] for p in st["probes"]] == [True], st
+
+
+def test_worker_killed_during_start_and_during_a_probe():
+    """a worker that dies while its generator is being built (model load / graph
+    capture) never reports; its pipe closes.  The supervisor thread must survive that at the
+    first start AND inside a re-probe, keep failing requests fast, and serve once the fault is
+    gone (the failed probe doubles the back-off)."""
+    import time
+    from cassmantle_amd.game.content import ImageGenerationError
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1"]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault")
+        open(trig, "w").close()
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:0", "CASSMANTLE_FAULT": "start_kill", "CASSMANTLE_FAULT_TRIGGER": trig}
+        sup = GroupSupervisor(_cfg(rooms), ["cpu:0"], rooms, gen_factory="cassmantle_amd.parallel.testing:stamped_generator",
+                              window_s=0.1, worker_env=env, start_timeout_s=240, reprobe_s=1.0)
+        try:
+            assert sup.wait_ready(240)
+            assert sup.live_devices() == [] and list(sup.retired) == ["cpu:0"]
+            t0 = time.time()
+            with pytest.raises(ImageGenerationError, match="repeats"):
+                sup.submit("", ["p"], [1]).result(timeout=30)
+            assert time.time() - t0 < 5
+            t_end = time.time() + 240                          # the first probe dies at start too
+            while not sup.probes and time.time() < t_end:
+                time.sleep(0.1)
+            assert sup.probes and sup.probes[0]["ok"] is False, sup.probes
+            os.remove(trig)
+            img, t_end = None, time.time() + 240
+            while img is None and time.time() < t_end:
+                try:
+                    img = sup.submit("1", ["p"], [2]).result(timeout=30)
+                except ImageGenerationError:
+                    time.sleep(0.2)
+            st = sup.status()
+        finally:
+            sup.close()
+    assert img is not None and slot_of(img[0]) == 0
+    assert [p["ok"] for p in st["probes"]][-1] is True and st["live_devices"] == ["cpu:0"], st
+    assert sup._probe_backoff == 1.0                           # reset by the first good round
+
+
+def test_weighted_ownership_and_slow_worker_does_not_hold_fast_rooms():
+    """verdict r4 item 2: the device shared with the front-end's scorer owns fewer rooms
+    (``weights``), and with async dispatch a straggler GPU does not delay the other GPUs' rooms:
+    the fast worker's rooms complete, and run further rounds, while the slow one still draws."""
+    import time
+    from cassmantle_amd.parallel.rooms import RoomSharding
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    sh = RoomSharding([str(i) for i in range(8)], 2, weights=[0.6, 1.0])
+    assert [len(sh.rooms_of(r)) for r in (0, 1)] == [3, 5]
+    assert RoomSharding([str(i) for i in range(5)], 3).rooms_of(0) == ["0", "3"]   # equal: round robin
+    rooms = [str(i) for i in range(8)]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault")
+        open(trig, "w").close()
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:0", "CASSMANTLE_FAULT": "slow", "CASSMANTLE_FAULT_DELAY": "3.0",
+               "CASSMANTLE_FAULT_TRIGGER": trig}
+        sup = GroupSupervisor(_cfg(rooms), ["cpu:0", "cpu:1"], rooms,
+                              gen_factory="cassmantle_amd.parallel.testing:stamped_generator", window_s=0.2,
+                              worker_env=env, start_timeout_s=240, weights={"cpu:0": 0.6})
+        try:
+            assert sup.wait_ready(240)
+            owners = sup.status()["owners"]
+            slow_rooms = {r for r, dv in owners.items() if dv == "cpu:0"}
+            fast_rooms = set(rooms) - slow_rooms
+            assert len(slow_rooms) == 3 and len(fast_rooms) == 5
+            t0 = time.monotonic()
+            done_at = {}
+            futs = {r: sup.submit(r, [f"p{r}"], [1]) for r in rooms}
+            for r, f in futs.items():
+                f.add_done_callback(lambda _f, r=r: done_at.setdefault(r, time.monotonic() - t0))
+            for f in futs.values():
+                f.result(timeout=120)
+            # while the slow worker is busy, the fast one serves more rounds of its own rooms
+            t1 = time.monotonic()
+            slow = {r: sup.submit(r, [f"q{r}"], [2]) for r in slow_rooms}
+            fast_rounds = 0
+            while not all(f.done() for f in slow.values()):
+                for r in fast_rooms:
+                    img = sup.submit(r, [f"f{r}"], [3]).result(timeout=60)
+                    assert slot_of(img[0]) == 1
+                fast_rounds += 1
+            slow_wall = time.monotonic() - t1
+            st = sup.status()
+        finally:
+            sup.close()
+    assert max(done_at[r] for r in fast_rooms) < 2.0 < min(done_at[r] for r in slow_rooms), done_at
+    assert fast_rounds >= 3 and slow_wall >= 3.0, (fast_rounds, slow_wall)
+    assert st["dispatch"] == "async" and st["worker_rounds"]["cpu:1"] > st["worker_rounds"]["cpu:0"], st

@@ -70,6 +70,12 @@ def parse():
                     help="as serve.py's GameConfig.score_topology: rank-0 scoring, or micro-batches of "
                          ">= --shard-min pairs split over every rank (C1 broadcast + C3 gather, parallel/scoring.py)")
     ap.add_argument("--shard-min", type=int, default=256)
+    ap.add_argument("--dispatch", choices=("async", "lockstep"), default="async",
+                    help="supervised topology: per-worker (async) or collective (lockstep) rounds")
+    ap.add_argument("--weight0", type=float, default=None,
+                    help="room share of GPU 0 (the scorer's device); default config.frontend_device_weight")
+    ap.add_argument("--slots-per-gpu", type=int, default=1,
+                    help="supervised workers per GPU (>1 runs gloo; a one-GPU rehearsal of several workers)")
     ap.add_argument("--gpus", type=int, default=None,
                     help="supervised topology on this many devices (front-end + one worker process each)")
     return ap.parse_args()
@@ -108,7 +114,9 @@ def main_supervised(a) -> None:
 
     gpu = torch.cuda.device_count() > 0          # (does not initialise the GPU on this image)
     n = a.gpus
-    devices = [f"cuda:{i}" for i in range(n)] if gpu else [f"cpu:{i}" for i in range(n)]
+    devices = ([f"cuda:{i}" + (f"#{k}" if k else "") for i in range(n) for k in range(a.slots_per_gpu)] if gpu
+               else [f"cpu:{i}" for i in range(n * a.slots_per_gpu)])
+    n = len(devices)
     spec = SPECS[a.model]
     cfg = Config()
     cfg.model.image_model = a.model
@@ -119,7 +127,9 @@ def main_supervised(a) -> None:
     cfg.model.device = "cuda" if gpu else "cpu"
     rooms = [""] + [str(i) for i in range(1, n)]
     t_start = time.perf_counter()
-    sup = GroupSupervisor(cfg, devices, rooms, window_s=0.05, start_timeout_s=1200)
+    w0 = cfg.game.frontend_device_weight if a.weight0 is None else a.weight0
+    sup = GroupSupervisor(cfg, devices, rooms, window_s=0.05, start_timeout_s=1200, dispatch=a.dispatch,
+                          weights={devices[0]: w0})
     if not sup.wait_ready(1500) or not sup.live_devices():
         raise SystemExit(f"worker group did not start: {sup.status()}")
     print(f"[live] worker group up on {sup.live_devices()} in {time.perf_counter() - t_start:.1f} s",
@@ -148,23 +158,33 @@ def main_supervised(a) -> None:
     print(f"[live] idle phase done: {len(idle)} requests", file=sys.stderr, flush=True)
     done = {"images": 0, "rounds": 0}
     stop = threading.Event()
+    mu = threading.Lock()
 
-    def gen_loop():
+    def room_loop(i, room):
+        # every room runs its own rounds (as the game's rooms do: each buffers its next content on
+        # its own timer), so a room on a fast GPU is never held by a room on a slow one
         step = 1
         while not stop.is_set():
-            done["images"] += one_round(step)
-            done["rounds"] += 1
+            f = sup.submit(room, prompts(step, i), [i * 10000 + step * 10 + j for j in range(a.batch)])
+            k = len(f.result(timeout=1800))
+            with mu:
+                done["images"] += k
+                done["rounds"] += 1
+                if i == 0:
+                    print(f"[live] {done['images']} images", file=sys.stderr, flush=True)
             step += 1
-            print(f"[live] {done['images']} images", file=sys.stderr, flush=True)
 
-    th = threading.Thread(target=gen_loop, daemon=True)
+    ths = [threading.Thread(target=room_loop, args=(i, room), daemon=True) for i, room in enumerate(rooms)]
     t0 = time.perf_counter()
-    th.start()
+    for th in ths:
+        th.start()
     load = asyncio.run(run_players(scorer, a.players, a.seconds, a.think_ms, 7))
-    imgs_at_stop = done["images"]
+    with mu:
+        imgs_at_stop = done["images"]
     elapsed = time.perf_counter() - t0
     stop.set()
-    th.join()
+    for th in ths:
+        th.join()
     st = sup.status()
     sup.close()
 
@@ -172,12 +192,13 @@ def main_supervised(a) -> None:
         return float(np.percentile(np.asarray(x), q)) if x else float("nan")
     print(json.dumps({
         "metric": "live round: images/s with overlapped streaming guess scoring (BASELINE config 5)",
-        "topology": "supervised", "images_per_s": round(imgs_at_stop / elapsed, 3), "n_gpus": n,
+        "topology": "supervised", "images_per_s": round(imgs_at_stop / elapsed, 3), "n_gpus": a.gpus, "workers": n,
         "devices": st["live_devices"], "players": a.players, "think_ms": a.think_ms,
         "idle_p50_ms": round(pct(idle, 50), 3), "idle_p99_ms": round(pct(idle, 99), 3),
         "load_p50_ms": round(pct(load, 50), 3), "load_p99_ms": round(pct(load, 99), 3), "requests": len(load),
         "rounds": done["rounds"], "gather_us_p50": st["gather_us_p50"], "retired": st["retired"],
-        "scorer_stream_priority": prio, "seconds": a.seconds,
+        "scorer_stream_priority": prio, "seconds": a.seconds, "dispatch": a.dispatch,
+        "worker_rounds": st.get("worker_rounds"),
         "config": {"model": a.model, "batch_per_room": a.batch, "rooms": len(rooms)}}), flush=True)
 
 
