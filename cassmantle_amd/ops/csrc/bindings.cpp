@@ -558,7 +558,7 @@ std::vector<at::Tensor> cosine_topk(const at::Tensor& table, const at::Tensor& v
   auto idx = at::empty({k}, table.options().dtype(at::kLong));
   launch_cosine_topk(table.data_ptr(), tf, V, (int)table.size(1), vec.data_ptr(), vf, (int)k,
                      reinterpret_cast<unsigned long long*>(ws.data_ptr<int64_t>()), vals.data_ptr<float>(),
-                     idx.data_ptr<int64_t>(), cur_stream());
+                     reinterpret_cast<long long*>(idx.data_ptr<int64_t>()), cur_stream());
   return {vals, idx};
 }
 

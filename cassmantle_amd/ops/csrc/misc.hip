@@ -74,6 +74,93 @@ __global__ void cosine_gemv_kernel(const void* __restrict__ table, int V, int D,
   if (lane == 0) out[row] = dot / fmaxf(sqrtf(nt) * sqrtf(nv), 1e-12f);
 }
 
+// ---------------------------------------------------------------- K15: cosine GEMV + top-k
+// most_similar (reference src/backend.py:297-301: wv.most_similar(word, topn=50)) over a V x D
+// word-vector table (V up to 3 M, D = 300).  No score vector goes to HBM and no library sort:
+//  pass 1 (topk_partial_kernel): a block scores TK_CHUNK consecutive rows (one wave per row,
+//         fp32 accumulation), keeps the scores in LDS as 64-bit keys {orderable(score), ~row},
+//         bitonic-sorts them descending and writes its best k keys;
+//  pass 2.. (topk_merge_kernel): the same sort over TK_CHUNK candidates per block until one
+//         block is left, which decodes the k best into (score, row) -- torch.topk's outputs.
+// The key order is total: equal scores rank the LOWER row first (deterministic ties).
+constexpr int TK_CHUNK = 2048;
+constexpr int TK_THREADS = 1024;
+
+CM_DEVICE uint32_t f_orderable(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+CM_DEVICE float f_from_orderable(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+CM_DEVICE unsigned long long tk_key(float score, int row) {
+  return ((unsigned long long)f_orderable(score) << 32) | (unsigned long long)(~(uint32_t)row);
+}
+
+// descending bitonic sort of TK_CHUNK keys in LDS by TK_THREADS threads (one pair each per step)
+CM_DEVICE void tk_sort_desc(unsigned long long* s) {
+  const int t = threadIdx.x;
+  for (int size = 2; size <= TK_CHUNK; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      const int i = 2 * t - (t & (stride - 1));
+      const int j = i + stride;
+      const bool down = (i & size) == 0;          // this pair's run is sorted descending
+      const unsigned long long a = s[i], b = s[j];
+      if ((a < b) == down) { s[i] = b; s[j] = a; }
+    }
+  }
+  __syncthreads();
+}
+
+template <bool TF32, bool VF32>
+__global__ void __launch_bounds__(TK_THREADS) topk_partial_kernel(const void* __restrict__ table, int V, int D,
+                                                                 const void* __restrict__ vec, int k,
+                                                                 unsigned long long* __restrict__ cand) {
+  __shared__ unsigned long long s[TK_CHUNK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int WAVES = TK_THREADS / 64, ROWS = TK_CHUNK / WAVES;
+  float nv = 0.f;
+  for (int c = lane; c < D; c += 64) { const float y = ld<VF32>(vec, c); nv = fmaf(y, y, nv); }
+  nv = sqrtf(wave_sum(nv));
+  const long long base = (long long)blockIdx.x * TK_CHUNK;
+  for (int i = 0; i < ROWS; ++i) {
+    const int slot = w * ROWS + i;
+    const long long row = base + slot;
+    unsigned long long key = 0ull;                 // below every real score: padding sorts last
+    if (row < V) {
+      float dot = 0.f, nt = 0.f;
+      for (int c = lane; c < D; c += 64) {
+        const float x = ld<TF32>(table, row * D + c), y = ld<VF32>(vec, c);
+        dot = fmaf(x, y, dot); nt = fmaf(x, x, nt);
+      }
+      dot = wave_sum(dot); nt = wave_sum(nt);
+      key = tk_key(dot / fmaxf(sqrtf(nt) * nv, 1e-12f), (int)row);
+    }
+    if (lane == 0) s[slot] = key;
+  }
+  tk_sort_desc(s);
+  for (int j = threadIdx.x; j < k; j += TK_THREADS) cand[(long long)blockIdx.x * k + j] = s[j];
+}
+
+__global__ void __launch_bounds__(TK_THREADS) topk_merge_kernel(const unsigned long long* __restrict__ in, int n, int k,
+                                                               unsigned long long* __restrict__ out,
+                                                               float* __restrict__ vals, long long* __restrict__ idx) {
+  __shared__ unsigned long long s[TK_CHUNK];
+  const long long base = (long long)blockIdx.x * TK_CHUNK;
+  for (int j = threadIdx.x; j < TK_CHUNK; j += TK_THREADS) s[j] = base + j < n ? in[base + j] : 0ull;
+  tk_sort_desc(s);
+  for (int j = threadIdx.x; j < k; j += TK_THREADS) {
+    const unsigned long long key = s[j];
+    if (vals != nullptr) {                         // last pass: decode (score, row)
+      vals[j] = f_from_orderable((uint32_t)(key >> 32));
+      idx[j] = (long long)(~(uint32_t)(key & 0xffffffffull));
+    } else {
+      out[(long long)blockIdx.x * k + j] = key;
+    }
+  }
+}
+
 __global__ void mean_pool_l2_kernel(const uint16_t* __restrict__ h, const int* __restrict__ lens,
                                     float* __restrict__ out, int T, int D) {
   extern __shared__ float buf[];   // [D] + [64]
@@ -425,93 +512,6 @@ void launch_cosine_topk(const void* table, int table_f32, int V, int D, const vo
 
 void launch_mean_pool_l2(const uint16_t* h, const int* lens, float* out, int B, int T, int D, hipStream_t s) {
   hipLaunchKernelGGL(mean_pool_l2_kernel, dim3(B), dim3(256), (D + 64) * sizeof(float), s, h, lens, out, T, D);
-}
-
-// ---------------------------------------------------------------- K15: cosine GEMV + top-k
-// most_similar (reference src/backend.py:297-301: wv.most_similar(word, topn=50)) over a V x D
-// word-vector table (V up to 3 M, D = 300).  No score vector goes to HBM and no library sort:
-//  pass 1 (topk_partial_kernel): a block scores TK_CHUNK consecutive rows (one wave per row,
-//         fp32 accumulation), keeps the scores in LDS as 64-bit keys {orderable(score), ~row},
-//         bitonic-sorts them descending and writes its best k keys;
-//  pass 2.. (topk_merge_kernel): the same sort over TK_CHUNK candidates per block until one
-//         block is left, which decodes the k best into (score, row) -- torch.topk's outputs.
-// The key order is total: equal scores rank the LOWER row first (deterministic ties).
-constexpr int TK_CHUNK = 2048;
-constexpr int TK_THREADS = 1024;
-
-CM_DEVICE uint32_t f_orderable(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-CM_DEVICE float f_from_orderable(uint32_t o) {
-  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
-}
-CM_DEVICE unsigned long long tk_key(float score, int row) {
-  return ((unsigned long long)f_orderable(score) << 32) | (unsigned long long)(~(uint32_t)row);
-}
-
-// descending bitonic sort of TK_CHUNK keys in LDS by TK_THREADS threads (one pair each per step)
-CM_DEVICE void tk_sort_desc(unsigned long long* s) {
-  const int t = threadIdx.x;
-  for (int size = 2; size <= TK_CHUNK; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      const int i = 2 * t - (t & (stride - 1));
-      const int j = i + stride;
-      const bool down = (i & size) == 0;          // this pair's run is sorted descending
-      const unsigned long long a = s[i], b = s[j];
-      if ((a < b) == down) { s[i] = b; s[j] = a; }
-    }
-  }
-  __syncthreads();
-}
-
-template <bool TF32, bool VF32>
-__global__ void __launch_bounds__(TK_THREADS) topk_partial_kernel(const void* __restrict__ table, int V, int D,
-                                                                 const void* __restrict__ vec, int k,
-                                                                 unsigned long long* __restrict__ cand) {
-  __shared__ unsigned long long s[TK_CHUNK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int WAVES = TK_THREADS / 64, ROWS = TK_CHUNK / WAVES;
-  float nv = 0.f;
-  for (int c = lane; c < D; c += 64) { const float y = ld<VF32>(vec, c); nv = fmaf(y, y, nv); }
-  nv = sqrtf(wave_sum(nv));
-  const long long base = (long long)blockIdx.x * TK_CHUNK;
-  for (int i = 0; i < ROWS; ++i) {
-    const int slot = w * ROWS + i;
-    const long long row = base + slot;
-    unsigned long long key = 0ull;                 // below every real score: padding sorts last
-    if (row < V) {
-      float dot = 0.f, nt = 0.f;
-      for (int c = lane; c < D; c += 64) {
-        const float x = ld<TF32>(table, row * D + c), y = ld<VF32>(vec, c);
-        dot = fmaf(x, y, dot); nt = fmaf(x, x, nt);
-      }
-      dot = wave_sum(dot); nt = wave_sum(nt);
-      key = tk_key(dot / fmaxf(sqrtf(nt) * nv, 1e-12f), (int)row);
-    }
-    if (lane == 0) s[slot] = key;
-  }
-  tk_sort_desc(s);
-  for (int j = threadIdx.x; j < k; j += TK_THREADS) cand[(long long)blockIdx.x * k + j] = s[j];
-}
-
-__global__ void __launch_bounds__(TK_THREADS) topk_merge_kernel(const unsigned long long* __restrict__ in, int n, int k,
-                                                               unsigned long long* __restrict__ out,
-                                                               float* __restrict__ vals, long long* __restrict__ idx) {
-  __shared__ unsigned long long s[TK_CHUNK];
-  const long long base = (long long)blockIdx.x * TK_CHUNK;
-  for (int j = threadIdx.x; j < TK_CHUNK; j += TK_THREADS) s[j] = base + j < n ? in[base + j] : 0ull;
-  tk_sort_desc(s);
-  for (int j = threadIdx.x; j < k; j += TK_THREADS) {
-    const unsigned long long key = s[j];
-    if (vals != nullptr) {                         // last pass: decode (score, row)
-      vals[j] = f_from_orderable((uint32_t)(key >> 32));
-      idx[j] = (long long)(~(uint32_t)(key & 0xffffffffull));
-    } else {
-      out[(long long)blockIdx.x * k + j] = key;
-    }
-  }
 }
 
 constexpr int BLUR_TS = 32;
