@@ -589,6 +589,13 @@ def pack_kv_fp8(k: torch.Tensor, v: torch.Tensor, kv_lens: Optional[torch.Tensor
 FP8_ATTN_VARIANTS = ("8x1", "4x1", "4x2", "2x2", "2x4", "1x4")
 
 
+def set_attention_d40_variant(variant: Optional[str]) -> None:
+    """Head dim 40 (SD-1.5 level 1): ``"16x16"`` (default) or ``"32x32"`` kernel; None restores
+    the default (``CASSMANTLE_ATTN16``).  A/B knob for tests and tools/bench_attn.py."""
+    if ext_available():
+        ext().set_attn_d40_variant({None: -1, "16x16": 1, "32x32": 0}[variant])
+
+
 def set_fp8_attention_variant(variant: Optional[str]) -> None:
     """Force the fp8 attention kernel's block shape ("NQxNS": NQ query groups of 32 x NS key
     splits per block; one of FP8_ATTN_VARIANTS) or restore the shape rule (None)."""

@@ -405,6 +405,278 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
   }
 }
 
+// ======================================================================= head dim 40, 16x16 MFMAs
+// The SD-1.5 level-1 attention (d = 40) on the 32x32x16 kernel above pays for P.V over 64 O^T
+// rows (40 real + ones column + 23 zero rows: 37.5 % of its MFMA cycles are padding).  Here every
+// product is a 16x16 block, so O^T needs only 48 rows (3 blocks):
+//   S^T[16 keys][16 q] = K . Q^T     two 16x16x32 steps: d 0..31, then d 32..39 plus the -m
+//                                    column (K[:, 40] = 1, Q^T[40][q] = -m, as above)
+//   O^T[16 d][16 q] += V^T . P^T     16x16x32 over 32 keys; P^T straight from the S accumulators
+//                                    of two 16-key blocks (k order permuted, see below), V^T by
+//                                    ds_read_b64_tr_b16 of the row-major V tile (T10)
+// Per wave: 32 queries (two 16-query blocks), 64-key tiles: QK^T 8 x 2 and P.V 12 16x16x32 MFMAs,
+// the 448 cycles per tile of the 32x32 layout, but on the 16x16 shape (MI355X_MICROARCH.md DVFS
+// item 7: the chip holds a higher clock on it) and with no padded O^T rows.  Lane l (g = l >> 4, i = l & 15) holds
+// S^T[key 16 kb + 4 g + r][query 16 qb + i], r = 0..3: a query's 64 keys sit in 4 lanes x 16
+// registers.  The deferred-max test only needs each lane's OWN max (all lanes <= THR <=> every
+// query's max <= THR), so the common tile has no cross-lane op; a rescale reduces over the 4
+// lanes (xor 16, xor 32).  The P.V contraction index k = 8 g + j of a k-step s pairs
+//   B = P^T: element j of lane (g, q) = P[q][32 s + 16 (j >> 2) + 4 g + (j & 3)]  (S registers)
+//   A = V^T: element j of lane (g, d) = V[32 s + 16 (j >> 2) + 4 g + (j & 3)][d]  (two tr reads)
+// Row sums come out of O^T row 40 (V[:, 40] = 1), rescaled with O for free.  Column 40 of K and
+// V (1.0) and 41..47 (0) are written once per LDS buffer; only d 0..39 is staged per tile.
+constexpr int A16_STR = 48;          // LDS row (elements): conflict-free b128 K reads and V tr reads
+constexpr int A16_NCH = 5;           // staged 16-B chunks per key row (d = 40)
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
+  constexpr int THREADS = 64 * NW;
+  constexpr int QB = 32 * NW;
+  constexpr int TILE = KT * A16_STR;   // elements of one K (or V) tile
+  constexpr int BUF = 2 * TILE;        // K + V
+  constexpr int CH = KT * A16_NCH;     // 16-B chunks per operand per tile
+  constexpr int LD = (CH + THREADS - 1) / THREADS;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+
+  const int nqb = (a.Nq + QB - 1) / QB;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = bid % nqb;
+  const int bh = bid / nqb;
+  const int h = bh % a.H;
+  const int b = bh / a.H;
+  const int q0 = qblk * QB + wave * 32;
+
+  int nk = a.Nk;
+  if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
+  const int ntiles = (nk + KT - 1) / KT;
+
+  const uint16_t* Qp = a.q + (long long)b * a.q_sb + (long long)h * a.q_sh;
+  const int hk = a.group > 1 ? h / a.group : h;
+  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)hk * a.k_sh;
+  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)hk * a.v_sh;
+
+  // Q^T fragments of the two query blocks, pre-scaled by scale*log2(e) (S in log2 units).
+  // k-step 0: d 0..31 (lane group g: d 8g..8g+7).  k-step 1: group 0 = d 32..39, group 1 = the
+  // -m column (element 0) against K's constant chunk d 40..47, groups 2-3 zero (their K slots
+  // re-read that chunk; a zero Q slot makes them inert).  Both steps are 16x16x32 MFMAs chained
+  // on one accumulator: a 16x16x32 result fed straight into a 16x16x16 MFMA as its accumulator
+  // came out wrong (the compiler placed no wait between the two shapes), and the 16x16x16 form
+  // costs ~0.8 of a 16x16x32 on gfx950 (tools/mfma16_probe.hip), so it would save little anyway.
+  const float qs = a.scale * 1.4426950408889634f;
+  bf16x8_t qA[2], qB[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = q0 + 16 * qb + li;
+    uint4 v = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+    if (q < a.Nq) {
+      v = *reinterpret_cast<const uint4*>(Qp + (long long)q * a.q_sn + 8 * g);
+      if (g == 0) w = *reinterpret_cast<const uint4*>(Qp + (long long)q * a.q_sn + 32);
+    }
+    float f[8], e[8];
+    unpack8(v, f);
+    unpack8(w, e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { f[j] *= qs; e[j] *= qs; }
+    qA[qb] = as_bf16x8(pack8(f));
+    qB[qb] = as_bf16x8(pack8(e));
+  }
+
+  // the constant column chunk (d 40 = 1.0, 41..47 = 0) of every row of both buffers' K and V
+  for (int r = tid; r < 2 * 2 * KT; r += THREADS)
+    *reinterpret_cast<uint4*>(lds + r * A16_STR + 40) = make_uint4(0x3F80u, 0, 0, 0);
+
+  // staging: chunk c -> key c / 5, 16-B chunk c % 5 of d 0..39 (tile-invariant, decoded once)
+  uint4 kr[LD], vr[LD];
+  int c_key[LD], c_lds[LD];
+  long long c_ks[LD], c_vs[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int c = tid + i * THREADS;
+    const int key = c / A16_NCH, ch = c - key * A16_NCH;
+    c_key[i] = c < CH ? key : (1 << 30);
+    c_lds[i] = c < CH ? key * A16_STR + ch * 8 : -1;
+    c_ks[i] = (long long)key * a.k_sn + ch * 8;
+    c_vs[i] = (long long)key * a.v_sn + ch * 8;
+  }
+  auto gload = [&](int t) {
+    const int kbase = t * KT;
+    const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+      if (kbase + c_key[i] < nk) {
+        x = *reinterpret_cast<const uint4*>(Kp + ko + c_ks[i]);
+        y = *reinterpret_cast<const uint4*>(Vp + vo + c_vs[i]);
+      }
+      kr[i] = x;
+      vr[i] = y;
+    }
+  };
+  auto lstore = [&](int bo) {
+#pragma unroll
+    for (int i = 0; i < LD; ++i)
+      if (c_lds[i] >= 0) {
+        *reinterpret_cast<uint4*>(lds + bo + c_lds[i]) = kr[i];
+        *reinterpret_cast<uint4*>(lds + bo + TILE + c_lds[i]) = vr[i];
+      }
+  };
+
+  if (ntiles > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  if constexpr (NW == 8 && ATTN_PRIO) {
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+
+  f32x4_t oacc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) oacc[i][qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {0.f, 0.f};
+  constexpr float RESCALE_THR = 8.f;
+  // tr-read geometry: lane 4q'+p of a 16-lane group addresses row q', columns 4p..4p+3
+  const int tr_off = (4 * g + (li >> 2)) * A16_STR + 4 * (li & 3);
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = t + 1 < ntiles;
+    if (more) gload(t + 1);
+    const int bo = (t & 1) * BUF;
+    const uint16_t* Ks = lds + bo;
+    const uint16_t* Vs = lds + bo + TILE;
+
+    // ---- S^T - m for 64 keys x 32 queries
+    f32x4_t sacc[4][2];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const uint16_t* krow = Ks + (16 * kb + li) * A16_STR;
+      const bf16x8_t kA = as_bf16x8(*reinterpret_cast<const uint4*>(krow + 8 * g));
+      const bf16x8_t kB = as_bf16x8(*reinterpret_cast<const uint4*>(krow + (g == 0 ? 32 : 40)));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kA, qA[qb], z, 0, 0, 0);
+        sacc[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kB, qB[qb], z, 0, 0, 0);
+      }
+    }
+    const int kbase = t * KT;
+    if (kbase + KT > nk) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool bad = kbase + 16 * kb + 4 * g + r >= nk;
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            if (bad) sacc[kb][qb][r] = -INFINITY;
+        }
+    }
+
+    // ---- deferred-max online softmax (lane-local test, see above)
+    float mx[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m = fmaxf(m, sacc[kb][qb][r]);
+      mx[qb] = m;
+    }
+    if (__builtin_expect(t == 0 || !__all(fmaxf(mx[0], mx[1]) <= RESCALE_THR), 0)) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float m = fmaxf(mx[qb], __shfl_xor(mx[qb], 16, 64));
+        const float2 hm = both_halves(m);
+        m = fmaxf(hm.x, hm.y);
+        float delta = (t == 0) ? m : fmaxf(m, 0.f);
+        if (!(delta > -1e30f)) delta = 0.f;            // fully masked tile for this query
+        const float mn = (float)(__bf16)(m_run[qb] + delta);   // an MFMA operand: keep it bf16-exact
+        delta = mn - m_run[qb];
+        m_run[qb] = mn;
+        if (g == 1) qB[qb][0] = (__bf16)(-mn);
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) oacc[i][qb][r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sacc[kb][qb][r] -= delta;
+      }
+    }
+    // ---- P^T fragments: k-step s = key blocks 2s, 2s+1 of this lane's 4-key groups
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float p[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[r] = __builtin_amdgcn_exp2f(sacc[2 * s2][qb][r]);
+          p[4 + r] = __builtin_amdgcn_exp2f(sacc[2 * s2 + 1][qb][r]);
+        }
+        pf[s2][qb] = as_bf16x8(pack8(p));
+      }
+    // ---- O^T += V^T P^T over 48 d rows
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int db = 0; db < 3; ++db) {
+        const uint16_t* base = Vs + 32 * s2 * A16_STR + 16 * db + tr_off;
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(base));
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base + 16 * A16_STR));
+        typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+        s16x8_t vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          oacc[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2][qb], oacc[db][qb], 0, 0, 0);
+      }
+    // the other buffer was last read in tile t - 1, which every wave finished before the
+    // previous barrier
+    if (more) lstore(BUF - bo);
+    __syncthreads();
+  }
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l, l = O^T row 40 (lanes 32..47, register 0 of block 2)
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const float ls = __shfl(oacc[2][qb][0], 32 + li, 64);
+    const int q = q0 + 16 * qb + li;
+    if (q >= a.Nq) continue;
+    const float inv = ls > 0.f ? 1.f / ls : 0.f;
+    uint16_t* Op = a.o + (long long)b * a.o_sb + (long long)q * a.o_sn + (long long)h * a.o_sh;
+#pragma unroll
+    for (int db = 0; db < 3; ++db) {
+      const int dd = 16 * db + 4 * g;
+      if (dd < 40) {
+        uint2 w;
+        w.x = pack2(oacc[db][qb][0] * inv, oacc[db][qb][1] * inv);
+        w.y = pack2(oacc[db][qb][2] * inv, oacc[db][qb][3] * inv);
+        *reinterpret_cast<uint2*>(Op + dd) = w;
+      }
+    }
+  }
+}
+
+template <int NW>
+void launch_a16(const AttnArgs& a, hipStream_t s) {
+  const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
+  hipLaunchKernelGGL((attn16_d40_kernel<NW>), dim3(nqb * a.H * a.B), dim3(64 * NW), 0, s, a);
+}
+
 template <int DQK, int DO, int NW>
 void launch_t(const AttnArgs& a, hipStream_t s) {
   using G = AttnGeom<DQK, DO>;
@@ -800,10 +1072,26 @@ void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s,
   }
 }
 
+// d = 40 kernel: 1 = 16x16-block kernel, 0 = the 32x32x16 kernel, -1 = CASSMANTLE_ATTN16 (default 1)
+static int g_attn_d40_variant = -1;
+void set_attn_d40_variant(int v) { g_attn_d40_variant = v; }
+
 void launch_attention(const AttnArgs& a, hipStream_t s) {
   switch (a.d) {
     case 32: launch_nw<32, 32>(a, s); break;
-    case 40: launch_nw<48, 64>(a, s); break;
+    case 40: {
+      // 16x16-block kernel (round 5) unless CASSMANTLE_ATTN16=0 (A/B knob) or causal masking
+      static const int a16_env = [] { const char* e = getenv("CASSMANTLE_ATTN16"); return e ? atoi(e) : 1; }();
+      const int a16 = g_attn_d40_variant >= 0 ? g_attn_d40_variant : a16_env;
+      if (a16 && !a.causal) {
+        const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
+        if (blocks8 >= 512) launch_a16<8>(a, s);
+        else launch_a16<4>(a, s);
+      } else {
+        launch_nw<48, 64>(a, s);
+      }
+      break;
+    }
     case 64: launch_nw<64, 64>(a, s); break;
     case 80: launch_nw<80, 96>(a, s); break;
     case 128: launch_nw<128, 128>(a, s); break;

@@ -850,6 +850,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("finalize_latents", &finalize_latents, nogil());
   m.def("dcopy", &dcopy, nogil());
   m.def("set_fp8_attn_variant", [](int64_t v) { set_fp8_attn_variant((int)v); });
+  m.def("set_attn_d40_variant", [](int64_t v) { set_attn_d40_variant((int)v); });
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());

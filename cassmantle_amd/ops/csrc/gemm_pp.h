@@ -111,7 +111,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
   const int nN = GEGLU ? (p.N + BN / 2 - 1) / (BN / 2) : (p.N + BN - 1) / BN;
   const int nM = (p.M + BM - 1) / BM;
   const int lin = xcd_remap(blockIdx.x, nN * nM);
-  const int tn = lin % nN, tm = lin / nN;
+  int tn, tm;
+  tile_of(lin, nM, nN, tm, tn);
   const int batch = blockIdx.z;
   const int m0 = tm * BM;
   const int n0 = GEGLU ? tn * (BN / 2) : tn * BN;

@@ -111,6 +111,7 @@ long long attention_fp8_workspace(const AttnArgs& a, int Hk);
 // packed = true: ws already holds K8/V8t of these K/V (attention_fp8_pack once per text
 // context for cross-attention), only the attention kernel runs
 void set_fp8_attn_variant(int v);
+void set_attn_d40_variant(int v);
 void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed = false);
 void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s);
 

@@ -318,6 +318,8 @@ def test_layer_norm(D, rows):
     (3, 16, 16, 12, 32, False),
     (1, 64, 64, 8, 160, False),
     (1, 4096, 4096, 8, 40, False),
+    (2, 4096, 77, 8, 40, False),                 # level-1 cross-attention (ragged last key tile)
+    (3, 200, 130, 2, 40, False),
 ])
 def test_attention(B, Nq, Nk, H, d, causal):
     q = rnd(B, Nq, H, d, seed=25)
@@ -1024,3 +1026,26 @@ def test_cosine_topk_in_tree(V, D, k, dtype):
         top = [q, V // 3, V // 2, V - 1]
         assert i[:4].tolist() == sorted(top), i[:8]
         assert torch.equal(v[:4], v[:1].expand(4))
+
+
+@pytest.mark.parametrize("variant", ["16x16", "32x32"])
+@pytest.mark.parametrize("B,Nq,Nk,H,lens,qscale", [(2, 4096, 4096, 8, None, 1.0), (2, 1000, 77, 8, None, 1.0),
+                                                   (3, 333, 200, 4, [200, 77, 3], 1.0),
+                                                   (2, 512, 512, 8, None, 6.0)])   # large scores: rescale path
+def test_attention_d40_kernels(variant, B, Nq, Nk, H, lens, qscale):
+    """head dim 40 (SD-1.5 level 1) on both kernels: the 16x16-block kernel (O^T over 48 rows,
+    P^T from the S accumulators, V^T by transposed LDS reads) and the 32x32x16 kernel, on strided
+    Q/K/V views of a fused QKV tensor, ragged key tiles, kv_lens and deferred-max rescales"""
+    d = 40
+    qkv = rnd(B, Nq, 3, H, d, seed=90)
+    q = qkv[:, :, 0] * qscale
+    kv = rnd(B, Nk, 2, H, d, seed=91)
+    k, v = kv[:, :, 0], kv[:, :, 1]
+    kl = torch.tensor(lens, dtype=torch.int32, device=DEV) if lens else None
+    ops.set_attention_d40_variant(variant)
+    try:
+        out = ops.attention(qkv[:, :, 0] if qscale == 1.0 else q, k, v, kv_lens=kl)
+    finally:
+        ops.set_attention_d40_variant(None)
+    exp = ref.attention(q, k, v, kv_lens=kl)
+    assert rel_err(out, exp) < 2e-2

@@ -45,15 +45,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only-d", type=int, default=None)
     a = ap.parse_args()
     ops.set_mode("hip")
     for B, Nq, Nk, H, d in SHAPES:
+        if a.only_d is not None and d != a.only_d:
+            continue
         g = torch.Generator(device="cuda").manual_seed(0)
         q = torch.randn(B, Nq, H, d, device="cuda", generator=g).to(torch.bfloat16)
         k = torch.randn(B, Nk, H, d, device="cuda", generator=g).to(torch.bfloat16)
         v = torch.randn(B, Nk, H, d, device="cuda", generator=g).to(torch.bfloat16)
         arms = {"bf16": lambda: ops.attention(q, k, v),
                 "sdpa": lambda: F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2))}
+        if d == 40:                        # the 32x32x16 kernel the 16x16 one replaced (A/B)
+            def old_kernel():
+                ops.set_attention_d40_variant("32x32")
+                ops.attention(q, k, v)
+                ops.set_attention_d40_variant(None)
+            arms["bf16_32x32"] = old_kernel
         if d == 64:
             arms["fp8"] = lambda: ops.attention(q, k, v, fp8="force")
             kv8 = ops.pack_kv_fp8(k, v)          # cross-attention: packed once per text context
@@ -66,6 +75,8 @@ def main():
         flops = 4.0 * B * H * Nq * Nk * d
         line = {"shape": [B, Nq, Nk, H, d], "us": med, "bf16_tflops": round(flops / med["bf16"] / 1e6, 1),
                 "bf16_vs_sdpa": round(med["sdpa"] / med["bf16"], 3)}
+        if "bf16_32x32" in med:
+            line["d40_16x16_vs_32x32"] = round(med["bf16_32x32"] / med["bf16"], 3)
         if "fp8" in med:
             line["fp8_vs_bf16"] = round(med["bf16"] / med["fp8"], 3)
             line["fp8_prepacked_vs_bf16"] = round(med["bf16"] / med["fp8_prepacked"], 3)

@@ -47,19 +47,30 @@ def main():
     ap.add_argument("--n", type=int, default=1280)
     ap.add_argument("--ks", default="64,128,256,640,1280,2560")
     ap.add_argument("--cfgs", default="3,0,13,16,21,22,23,8")
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="cycle through this many weight AND activation copies per replay (>= 40 at "
+                         "M 2048 x N 1280: every launch reads both from HBM, as a UNet eval does for weights)")
+    ap.add_argument("--splits", default="1,2,4")
     a = ap.parse_args()
     ops.set_mode("hip")
     ops.load_gemm_tuning()
     z = torch.zeros(256, device="cuda", dtype=torch.float32)
     print(json.dumps({"case": "empty zero_ kernel", "us": round(graph_time(lambda: ops.zero_(z)), 2)}), flush=True)
     for K in [int(k) for k in a.ks.split(",")]:
-        x = (torch.randn(a.m, K, device="cuda") * 0.5).to(torch.bfloat16)
-        w = (torch.randn(a.n, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+        xs = [(torch.randn(a.m, K, device="cuda") * 0.5).to(torch.bfloat16) for _ in range(a.rotate)]
+        ws = [(torch.randn(a.n, K, device="cuda") / K ** 0.5).to(torch.bfloat16) for _ in range(a.rotate)]
         b = torch.zeros(a.n, device="cuda", dtype=torch.bfloat16)
         out = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
+        it = [0]
+
+        def call():
+            i = it[0] % a.rotate
+            it[0] += 1
+            ops.linear(xs[i], ws[i], b, out=out)
+        x, w = xs[0], ws[0]
         row = {"M": a.m, "N": a.n, "K": K}
         for c in [int(c) for c in a.cfgs.split(",")]:
-            for sp in (1, 2, 4):
+            for sp in [int(v) for v in a.splits.split(",")]:
                 if sp > 1 and K // 64 // sp < 4:
                     continue
                 ext().gemm_set_override(c, sp)
@@ -67,9 +78,9 @@ def main():
                 got = tuple(ext().gemm_last_plan())
                 if got != (c, sp):
                     continue
-                row[f"{c}/{sp}"] = round(graph_time(lambda: ops.linear(x, w, b, out=out)), 2)
+                row[f"{c}/{sp}"] = round(graph_time(call, reps=max(20, a.rotate)), 2)
         ext().gemm_set_override(-1, 0)
-        row["auto"] = round(graph_time(lambda: ops.linear(x, w, b, out=out)), 2)
+        row["auto"] = round(graph_time(call, reps=max(20, a.rotate)), 2)
         row["auto_plan"] = list(ext().gemm_last_plan())
         print(json.dumps(row), flush=True)
 
