@@ -15,3 +15,4 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o r
 grep '^{' gpurun_out/prof_$name.log | head -c 400; echo
 f=$(find gpurun_out/prof_$name -name '*kernel_trace.csv' | head -1)
 python tools/prof_summary.py "$f" --per $per --top 60 > gpurun_out/prof_${name}_summary.txt && head -40 gpurun_out/prof_${name}_summary.txt
+python tools/prof_summary.py "$f" --last-gen --top 60 > gpurun_out/prof_${name}_steady.txt && head -30 gpurun_out/prof_${name}_steady.txt

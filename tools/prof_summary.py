@@ -16,9 +16,22 @@ def main():
     ap.add_argument("--per", type=float, default=1.0)
     ap.add_argument("--skip-before", default=None,
                     help="ignore kernels before the first one whose name contains this string")
+    ap.add_argument("--last-gen", action="store_true",
+                    help="steady state only: summarise the LAST generation (after the previous image's "
+                         "to_uint8 up to the last one), per UNet eval = per latent_step_kernel launch")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if a.last_gen:
+        ends = [i for i, r in enumerate(rows) if "to_uint8_kernel" in r["Kernel_Name"]]
+        if len(ends) >= 2:
+            rows = rows[ends[-2] + 1:ends[-1] + 1]
+        evals = sum("latent_step_kernel" in r["Kernel_Name"] for r in rows)
+        if evals:
+            a.per = float(evals)
+        span = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e6
+        print(f"steady state: last generation only, {len(rows)} launches, {evals} UNet evals, "
+              f"wall {span:.2f} ms first start -> last end")
     if a.skip_before:
         first = next((i for i, r in enumerate(rows) if a.skip_before in r["Kernel_Name"]), 0)
         rows = rows[first:]
