@@ -28,17 +28,21 @@ def main():
     vdir = os.path.join(B.BUILD, "variant")
     os.makedirs(vdir, exist_ok=True)
     srcs = dict(zip(a.file, a.src))
+    cmds = []
     for src in sorted(glob.glob(os.path.join(B.CSRC, "*.hip"))):
         name = os.path.basename(src)
         obj = os.path.join(B.BUILD, name + ".o")
         if name in a.file:
             alt = srcs.get(name, src)
             obj = os.path.join(vdir, name + ".o")
-            cmd = [hipcc, f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", "-O3", "-fPIC", "-std=c++17",
-                   f"-I{B.CSRC}", "-Wno-unused-result", "-Wno-unused-variable", "-mllvm",
-                   "-pragma-unroll-threshold=100000", *a.flags.split(), "-c", alt, "-o", obj]
-            subprocess.run(cmd, check=True)
+            cmds.append([hipcc, f"--offload-arch={B.ARCH}", "-munsafe-fp-atomics", "-O3", "-fPIC", "-std=c++17",
+                         f"-I{B.CSRC}", "-Wno-unused-result", "-Wno-unused-variable", "-mllvm",
+                         "-pragma-unroll-threshold=100000", *a.flags.split(), "-c", alt, "-o", obj])
         objs.append(obj)
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:   # the rebuilt units in parallel
+        for r in ex.map(lambda c: subprocess.run(c, check=True), cmds):
+            pass
     objs.append(os.path.join(B.BUILD, "bindings.o"))
     _, lib, _ = B._torch_paths()
     subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *objs, "-o", a.out, f"-L{lib}", "-lc10",
