@@ -37,7 +37,34 @@ long long* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N
   return reinterpret_cast<long long*>(t->data_ptr<int64_t>());
 }
 
+// tile raster group of every GEMM launch (gemm_impl.h tile_of): 0 = the compiled default;
+// separate values for gated (GEGLU / SwiGLU) calls.  CASSMANTLE_GEMM_RASTER="G" or "G,Ggated",
+// or gemm_set_raster at run time (A/B knob)
+static int g_raster[2] = {-1, -1};
+static void raster_from_env() {
+  static const bool once = [] {
+    const char* e = getenv("CASSMANTLE_GEMM_RASTER");
+    int a = 0, b = -1;
+    if (e != nullptr) {
+      if (sscanf(e, "%d,%d", &a, &b) < 2) b = a;
+    } else {
+      b = 0;
+    }
+    if (g_raster[0] < 0) g_raster[0] = a;
+    if (g_raster[1] < 0) g_raster[1] = b;
+    return true;
+  }();
+  (void)once;
+}
+void gemm_set_raster(int64_t plain, int64_t gated) {
+  raster_from_env();
+  g_raster[0] = (int)plain;
+  g_raster[1] = (int)gated;
+}
+
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
+  raster_from_env();
+  p.raster = g_raster[(p.act == 4 || p.act == 6) ? 1 : 0];   // gated: GEGLU (4) / SwiGLU (6)
   // output statistics are fused into the LDS-staged bf16 epilogue; shapes that take another
   // path (fp32 out, GEMV rows, batched, gated) get a separate per-channel statistics pass over
   // the output; split-K shapes accumulate them in the reduce pass
@@ -851,6 +878,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dcopy", &dcopy, nogil());
   m.def("set_fp8_attn_variant", [](int64_t v) { set_fp8_attn_variant((int)v); });
   m.def("set_attn_d40_variant", [](int64_t v) { set_attn_d40_variant((int)v); });
+  m.def("gemm_set_raster", &gemm_set_raster);
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());

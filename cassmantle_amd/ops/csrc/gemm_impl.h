@@ -51,19 +51,21 @@ constexpr int BK = 64;
 
 CM_DEVICE int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-// tile of linear (XCD-remapped) index lin: rows of N-tiles (G = 0: tm = lin / nN), or groups of G
-// M-tiles walked column by column (GEMM_RASTER_G = G), so the 32 consecutive tiles an XCD runs
-// cover G M-panels x 32/G N-panels instead of 2 x 16 (less A+W per XCD L2 on small grids).
-// G = 4 measured 524.9 -> 521.6 ms/step on the bench, same box x2 (profiles/r5_raster_ab.txt)
+// tile of linear (XCD-remapped) index lin: rows of N-tiles (G = 1: tm = lin / nN), or groups of G
+// M-tiles walked column by column, so the 32 consecutive tiles an XCD runs cover G M-panels x
+// 32/G N-panels instead of 2 x 16 (less A+W per XCD L2 on small grids).  G = p.raster, or
+// GEMM_RASTER_G when 0.  G = 4 measured 524.9 -> 521.6 ms/step on the bench, same box x2
+// (profiles/r5_raster_ab.txt)
 #ifndef GEMM_RASTER_G
 #define GEMM_RASTER_G 4
 #endif
-CM_DEVICE void tile_of(int lin, int nM, int nN, int& tm, int& tn) {
-  if constexpr (GEMM_RASTER_G > 1) {
-    const int grp = lin / (GEMM_RASTER_G * nN);
-    const int gs = min(GEMM_RASTER_G, nM - grp * GEMM_RASTER_G);
-    const int r = lin - grp * GEMM_RASTER_G * nN;
-    tm = grp * GEMM_RASTER_G + r % gs;
+CM_DEVICE void tile_of(int lin, int nM, int nN, int raster, int& tm, int& tn) {
+  const int G = min(raster > 0 ? raster : GEMM_RASTER_G, nM);
+  if (G > 1) {
+    const int grp = lin / (G * nN);
+    const int gs = min(G, nM - grp * G);
+    const int r = lin - grp * G * nN;
+    tm = grp * G + r % gs;
     tn = r / gs;
   } else {
     tn = lin % nN;
@@ -520,7 +522,7 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int nM = (p.M + BM - 1) / BM;
   const int lin = xcd_remap(blockIdx.x, nN * nM);
   int tn, tm;
-  tile_of(lin, nM, nN, tm, tn);
+  tile_of(lin, nM, nN, p.raster, tm, tn);
   const int batch = blockIdx.z;
   const int m0 = tm * BM;
   const int n0 = GEGLU ? tn * (BN / 2) : tn * BN;   // output-column origin

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, float* __re
   const int nM = (p.M + BM - 1) / BM;
   const int lin = xcd_remap(blockIdx.x, nN * nM);
   int tn, tm;
-  tile_of(lin, nM, nN, tm, tn);
+  tile_of(lin, nM, nN, p.raster, tm, tn);
   const int batch = blockIdx.z;
   const int m0 = tm * BM;
   const int n0 = GEGLU ? tn * (BN / 2) : tn * BN;

@@ -21,6 +21,7 @@ struct GemmArgs {
   int out_f32 = 0;
   int split = 1;                       // split-K slices (gemm_plan)
   int cfg = 0;                         // tile config index (gemm_plan)
+  int raster = 0;                      // tile raster group (gemm_impl.h tile_of; 0 = compiled default)
   // implicit-GEMM convolution (conv != 0)
   int conv = 0, IH = 0, IW = 0, Cin = 0, Ho = 0, Wo = 0, stride = 1, pad = 0, ksize = 1, upsample = 0;
   // parity-upsample conv (nearest-2x upsample + 3x3 conv as four 2x2 convs on the low-res input,
