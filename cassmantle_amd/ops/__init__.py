@@ -52,6 +52,10 @@ def _use_hip(t: torch.Tensor) -> bool:
 _TUNE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _RECORD: Optional[list] = None
 _tune_loaded = False
+# timing diagnostic only (results are WRONG: epilogue statistics accumulate twice):
+# CASSMANTLE_DIAG_TWICE=1 launches every GEMM / conv twice back to back, so a kernel trace shows
+# each call cold (operands as the pipeline leaves them) and then warm (tools/diag_twice.py)
+_DIAG_TWICE = os.environ.get("CASSMANTLE_DIAG_TWICE", "0") == "1"
 
 
 def load_gemm_tuning(path: Optional[str] = None) -> int:
@@ -91,6 +95,8 @@ def record_gemms(on: bool) -> Optional[list]:
 def _launch(fn, *args, **kw):
     if not _tune_loaded:
         load_gemm_tuning()
+    if _DIAG_TWICE:
+        fn(*args, **kw)
     fn(*args, **kw)
     if _RECORD is not None:
         call = lambda: fn(*args, **kw)   # noqa: E731

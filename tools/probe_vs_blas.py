@@ -16,6 +16,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cassmantle_amd import ops  # noqa: E402
+from cassmantle_amd.ops._ext import ext  # noqa: E402
 from tools.probe_small_gemm import graph_time  # noqa: E402
 
 SHAPES = ("2048x1280x1280,2048x1280x5120,2048x10240x1280,2048x3840x1280,8192x640x640,8192x5120x640,"
@@ -26,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default=SHAPES, help="MxNxK list")
     ap.add_argument("--rotate", type=int, default=4)
+    ap.add_argument("--cfgs", default="", help="also time the in-tree kernel forced to these cfg[:split] plans")
     a = ap.parse_args()
     ops.set_mode("hip")
     ops.load_gemm_tuning()
@@ -53,6 +55,15 @@ def main():
         y0 = ops.linear(xs[0], ws[0])
         y1 = torch.matmul(xs[0], ws[0].t())
         err = float((y0.float() - y1.float()).abs().max())
+        for cs in [c for c in a.cfgs.split(",") if c]:
+            cfg, _, sp = cs.partition(":")
+            ext().gemm_set_override(int(cfg), int(sp or 1))
+            try:
+                t_c = graph_time(ours, reps=reps, replays=5)
+                print(json.dumps({"shape": s, "cfg": cs, "us": round(t_c, 2), "tf": round(flop / t_c * 1e-6, 1)}), flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(json.dumps({"shape": s, "cfg": cs, "error": str(e)[:160]}), flush=True)
+            ext().gemm_set_override(-1, 0)
         print(json.dumps({"shape": s, "ours_us": round(t_ours, 2), "blas_us": round(t_blas, 2),
                           "ours_tf": round(flop / t_ours * 1e-6, 1), "blas_tf": round(flop / t_blas * 1e-6, 1),
                           "ratio": round(t_ours / t_blas, 3), "max_abs_diff": err}), flush=True)
