@@ -596,10 +596,11 @@ FP8_ATTN_VARIANTS = ("8x1", "4x1", "4x2", "2x2", "2x4", "1x4")
 
 
 def set_attention_d40_variant(variant: Optional[str]) -> None:
-    """Head dim 40 (SD-1.5 level 1): ``"16x16"`` (default) or ``"32x32"`` kernel; None restores
-    the default (``CASSMANTLE_ATTN16``).  A/B knob for tests and tools/bench_attn.py."""
+    """Head dim 40 (SD-1.5 level 1): ``"16x16"`` (default), ``"32x32"`` or ``"mixed"`` (32x32x16
+    QK^T, 16x16x32 P.V) kernel; None restores the default (``CASSMANTLE_ATTN16`` = 1 / 0 / 2).
+    A/B knob for tests and tools/bench_attn.py."""
     if ext_available():
-        ext().set_attn_d40_variant({None: -1, "16x16": 1, "32x32": 0}[variant])
+        ext().set_attn_d40_variant({None: -1, "16x16": 1, "32x32": 0, "mixed": 2}[variant])
 
 
 def set_fp8_attention_variant(variant: Optional[str]) -> None:

@@ -1028,7 +1028,7 @@ def test_cosine_topk_in_tree(V, D, k, dtype):
         assert torch.equal(v[:4], v[:1].expand(4))
 
 
-@pytest.mark.parametrize("variant", ["16x16", "32x32"])
+@pytest.mark.parametrize("variant", ["16x16", "32x32", "mixed"])
 @pytest.mark.parametrize("B,Nq,Nk,H,lens,qscale", [(2, 4096, 4096, 8, None, 1.0), (2, 1000, 77, 8, None, 1.0),
                                                    (3, 333, 200, 4, [200, 77, 3], 1.0),
                                                    (2, 512, 512, 8, None, 6.0)])   # large scores: rescale path

@@ -39,6 +39,8 @@ def mfma_flops(name: str) -> float:
         return 2 * 32 * 32 * 64
     if name.startswith(("attn_fwd", "attn_d512")):
         return 2 * 32 * 32 * 16
+    if name.startswith("attn_mx"):          # per 64-key tile: 6 x 32x32x16 + 12 x 16x16x32
+        return (6 * 2 * 32 * 32 * 16 + 12 * 2 * 16 * 16 * 32) / 18
     return 2 * 16 * 16 * 32
 
 
