@@ -902,14 +902,14 @@ constexpr int SK_QB = 16;                  // column quads per block
 constexpr int SK_RL = 256 / SK_QB;         // row lanes
 template <bool OUTF32>
 __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, const float* __restrict__ partial,
-                                                                  int split) {
+                                                                  int split, int rb) {
   __shared__ float red[2][SK_RL][SK_QB * 4];
   const int bz = blockIdx.z;
   partial += (long long)bz * split * p.M * p.N;
   const int qd = threadIdx.x % SK_QB, rl = threadIdx.x / SK_QB;
   const int n = (blockIdx.x * SK_QB + qd) * 4;
-  const int m0 = blockIdx.y * SK_RB;
-  const int m1 = min(p.M, m0 + SK_RB);
+  const int m0 = blockIdx.y * rb;
+  const int m1 = min(p.M, m0 + rb);
   const bool on = n < p.N;
   const int shw = p.stats_hw;
   const bool single = (m0 / shw) == ((m1 - 1) / shw);
@@ -985,8 +985,16 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(GemmArgs p, co
 template <bool OUTF32>
 void launch_splitk_reduce(const GemmArgs& p, float* ws, int split, hipStream_t s) {
   if (p.stats != nullptr) {
-    dim3 g2((unsigned)((p.N / 4 + SK_QB - 1) / SK_QB), (unsigned)((p.M + SK_RB - 1) / SK_RB), (unsigned)p.batch);
-    hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split);
+    // rows per block: SK_RB, halved (down to one row per row lane) while the grid has fewer than
+    // 512 blocks -- the small-M reduces (batch-1 levels 3 / 4: 160 blocks at M 512) are bound by
+    // each thread's serial rows, not by the statistics atomics that larger blocks save
+    // (CASSMANTLE_SK_ADAPT=0: fixed SK_RB, A/B knob)
+    static const int adapt = [] { const char* e = getenv("CASSMANTLE_SK_ADAPT"); return e ? atoi(e) : 1; }();
+    const long long cols = (p.N / 4 + SK_QB - 1) / SK_QB;
+    int rb = SK_RB;
+    while (adapt && rb > SK_RL && cols * ((p.M + rb - 1) / rb) * p.batch < 512) rb /= 2;
+    dim3 g2((unsigned)cols, (unsigned)((p.M + rb - 1) / rb), (unsigned)p.batch);
+    hipLaunchKernelGGL(splitk_reduce_stats_kernel<OUTF32>, g2, dim3(256), 0, s, p, ws, split, rb);
   } else {
     const long long nq = (long long)p.M * (p.N / 4);
     const long long nb = (nq + 255) / 256;
