@@ -330,6 +330,29 @@ def test_attention(B, Nq, Nk, H, d, causal):
     assert rel_err(out, exp) < 2e-2
 
 
+@pytest.mark.parametrize("B,Nq,Nk,H,d,lens", [
+    (8, 256, 256, 8, 160, None),                  # SD-1.5 level 3 at the bench batch
+    (2, 256, 256, 8, 160, None),                  # level 3 at batch 1 (64 two-wave blocks)
+    (2, 1024, 1024, 8, 80, None),                 # level 2 at batch 1
+    (8, 256, 77, 8, 160, None),                   # level-3 cross-attention
+    (1, 300, 1000, 2, 96, None),                  # 16 ragged key tiles
+    (3, 100, 300, 2, 128, [300, 70, 1]),          # kv_lens down to one key
+])
+def test_attention_short_grids(B, Nq, Nk, H, d, lens):
+    """the generic kernel on the short grids of batch 1 / level 3 (2-wave blocks) vs the fp32
+    reference.  (A key split over blocks with an fp32 partial merge was built for these grids in
+    round 5, passed this test, and measured 1.9x slower on the level-3 shape -- 35.0 vs 18.0 us --
+    and +8 ms per bench step: removed, profiles/r5_attn_key_split_negative.txt)"""
+    q = rnd(B, Nq, H, d, seed=71)
+    k = rnd(B, Nk, H, d, seed=72)
+    v = rnd(B, Nk, H, d, seed=73)
+    kl = torch.tensor(lens, dtype=torch.int32, device=DEV) if lens else None
+    out = ops.attention(q, k, v, kv_lens=kl)
+    exp = ref.attention(q, k, v, kv_lens=kl)
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out, exp) < 2e-2
+
+
 def test_attention_strided_qkv_and_kv_lens():
     B, N, H, d = 3, 20, 12, 32
     qkv = rnd(B, N, 3, H, d, seed=28)
