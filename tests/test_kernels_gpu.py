@@ -1054,7 +1054,8 @@ def test_cosine_topk_in_tree(V, D, k, dtype):
 @pytest.mark.parametrize("variant", ["16x16", "32x32", "mixed"])
 @pytest.mark.parametrize("B,Nq,Nk,H,lens,qscale", [(2, 4096, 4096, 8, None, 1.0), (2, 1000, 77, 8, None, 1.0),
                                                    (3, 333, 200, 4, [200, 77, 3], 1.0),
-                                                   (2, 512, 512, 8, None, 6.0)])   # large scores: rescale path
+                                                   (2, 512, 512, 8, None, 6.0),    # large scores: rescale path
+                                                   (3, 300, 1000, 2, [1000, 300, 5], 1.0)])   # key split, empty split
 def test_attention_d40_kernels(variant, B, Nq, Nk, H, lens, qscale):
     """head dim 40 (SD-1.5 level 1) on both kernels: the 16x16-block kernel (O^T over 48 rows,
     P^T from the S accumulators, V^T by transposed LDS reads) and the 32x32x16 kernel, on strided
