@@ -166,6 +166,36 @@ def test_sdxl_unet_reduced_depth_full_width(fp8):
     assert c >= (0.995 if fp8 else 0.999), c
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+def test_sdxl_chained_ln_row_stats_match_stats_pass(fp8):
+    """SDXL transformer stacks deeper than one block at >= 1024 rows (the 32^2 level of a 1024^2
+    image): block i's feed-forward output projection accumulates the row statistics of its
+    output for block i + 1's folded LayerNorm (unet._FF_ROWSTATS) -- same UNet output as the
+    row-statistics pass it replaces"""
+    import dataclasses
+    import cassmantle_amd.models.unet as U
+    cfg = dataclasses.replace(U.SDXL_UNET, transformer_depth=(0, 1, 3), mid_transformer_depth=2, sample_size=128)
+    m = U.UNet(cfg, seed=4).cuda()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(1, 128, 128, 4, generator=g).to(torch.bfloat16).cuda()
+    t = torch.tensor([500.0]).cuda()
+    ctx = (torch.randn(1, 77, 2048, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    added = {"time_ids": torch.tensor([[1024.0, 1024.0, 0.0, 0.0, 1024.0, 1024.0]]).cuda(),
+             "text_embeds": (torch.randn(1, 1280, generator=g) * 0.5).to(torch.bfloat16).cuda()}
+    old = U._FF_ROWSTATS
+    with torch.no_grad():
+        try:
+            U._FF_ROWSTATS = True
+            a = m(x, t, ctx, added, fp8=fp8).float()
+            U._FF_ROWSTATS = False
+            b = m(x, t, ctx, added, fp8=fp8).float()
+        finally:
+            U._FF_ROWSTATS = old
+    assert torch.isfinite(a).all()
+    c = cos(a.cpu(), b.cpu())
+    assert c >= 0.9999, c
+
+
 def test_fp8_cross_kv_survives_batch_size_change_under_graphs():
     """the e4m3 cross-attention K/V image must be kept per context shape.  A
     graph captured at B=1, then a generation at B=2, then a replay at B=1 must give exactly the
