@@ -40,6 +40,9 @@ constexpr int KT = 64;  // keys per tile
 #ifndef ATTN_PRIO
 #define ATTN_PRIO 1
 #endif
+#ifndef F8_ONES_SUM
+#define F8_ONES_SUM 1
+#endif
 
 // v_permlane32_swap of a value with itself: one of the two results is this lane's own value and
 // the other lane l ^ 32's (lanes 0-31 get it in .y, lanes 32-63 in .x), so a cross-half max or
@@ -1146,6 +1149,17 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m_run = 0.f, l_run = 0.f;
   constexpr float RESCALE_THR = 8.f;
+  // F8_ONES_SUM: the row sums of P come from one more MFMA per tile against an all-ones e4m3 A
+  // operand (every row of lsum = the query's sum over the tile's 64 keys, of the same fp8 P the
+  // P.V MFMAs use) instead of 32 VALU adds + a cross-half shuffle per tile.  Key-split variants
+  // only (the self-attention shapes): on the NS = 1 blocks (77-key cross-attention, 2 tiles) its
+  // 16 accumulator registers would cost a wave per SIMD (117 -> 132 registers)
+  constexpr bool ONES = F8_ONES_SUM && NS > 1;
+  f32x16_t lsum;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
+  const i32x8_t ones8 = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                         0x38383838, 0x38383838, 0x38383838, 0x38383838};   // e4m3 1.0
   const uint8_t* const Kw = Ks + ks * TILE_B;
   const uint8_t* const Vw = Vs + ks * TILE_B;
 
@@ -1191,6 +1205,10 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
         m_run += delta;
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         l_run *= alpha;
+        if constexpr (ONES) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1200,17 +1218,24 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
 #pragma unroll
           for (int r = 0; r < 16; ++r) sacc[hf][r] -= delta;
       }
-      float rs = 0.f;
+      if constexpr (ONES) {
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
+        for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
-          sacc[hf][r] = pv;
-          rs += pv;
-        }
-      rs += __shfl_xor(rs, 32, 64);
-      l_run += rs;
+          for (int r = 0; r < 16; ++r) sacc[hf][r] = __builtin_amdgcn_exp2f(sacc[hf][r]);
+      } else {
+        float rs = 0.f;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(sacc[hf][r]);
+            sacc[hf][r] = pv;
+            rs += pv;
+          }
+        rs += __shfl_xor(rs, 32, 64);
+        l_run += rs;
+      }
       // P^T fragment: element j = sacc[j >> 4][j & 15]
       i32x8_t pf;
 #pragma unroll
@@ -1226,6 +1251,8 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
         const i32x8_t vf = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
         oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
       }
+      if constexpr (ONES)
+        lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pf, lsum, 0, 0, 0, 127, 0, 127);
     }
     __syncthreads();
     if (more) {
@@ -1233,6 +1260,7 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
       __syncthreads();
     }
   }
+  if constexpr (ONES) l_run = lsum[0];
   if constexpr (NS > 1) {
     // merge the key splits: every wave is past the loop's last barrier, so the staging LDS is
     // free; splits 1.. publish (O, m, l) per lane (lane-contiguous records: no bank conflicts)
