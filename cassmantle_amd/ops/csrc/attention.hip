@@ -20,6 +20,8 @@
 // K/V tiles of 64 keys are staged global->registers->LDS with the next tile's loads issued
 // before the current tile's MFMAs (T14).  LDS strides are padded so the K row reads
 // (16 distinct rows per lane group) and the V transposed reads are bank-conflict-free.
+#include <atomic>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -1341,7 +1343,7 @@ void launch_attention_fp8_pack(const AttnArgs& a, int Hk, uint8_t* ws, hipStream
 }
 
 // forced fp8 variant NQ*10 + NS (0: the shape rule); set by ops.set_fp8_attention_variant
-static int g_fp8_attn_variant = 0;
+static std::atomic<int> g_fp8_attn_variant{0};   // A/B knob, read by every launch thread
 void set_fp8_attn_variant(int v) { g_fp8_attn_variant = v; }
 
 void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s, bool packed) {
@@ -1357,7 +1359,8 @@ void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s,
     int nq = 0, ns = 0;
     return sscanf(e, "%dx%d", &nq, &ns) == 2 ? nq * 10 + ns : 0;
   }();
-  const int forced = g_fp8_attn_variant > 0 ? g_fp8_attn_variant : env_forced;
+  const int fv = g_fp8_attn_variant.load(std::memory_order_relaxed);
+  const int forced = fv > 0 ? fv : env_forced;
   const long long groups = (long long)((a.Nq + 31) / 32) * a.H * a.B;
   const int nkt = (a.Nk + KT - 1) / KT;
   int v = forced;
@@ -1377,7 +1380,7 @@ void launch_attention_fp8(const AttnArgs& a, int Hk, uint8_t* ws, hipStream_t s,
 }
 
 // d = 40 kernel: 1 = 16x16-block kernel, 0 = the 32x32x16 kernel, -1 = CASSMANTLE_ATTN16 (default 1)
-static int g_attn_d40_variant = -1;
+static std::atomic<int> g_attn_d40_variant{-1};   // A/B knob, read by every launch thread
 void set_attn_d40_variant(int v) { g_attn_d40_variant = v; }
 
 void launch_attention(const AttnArgs& a, hipStream_t s) {
@@ -1386,7 +1389,8 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     case 40: {
       // 16x16-block kernel (round 5) unless CASSMANTLE_ATTN16=0 (A/B knob) or causal masking
       static const int a16_env = [] { const char* e = getenv("CASSMANTLE_ATTN16"); return e ? atoi(e) : 1; }();
-      const int a16 = g_attn_d40_variant >= 0 ? g_attn_d40_variant : a16_env;
+      const int dv = g_attn_d40_variant.load(std::memory_order_relaxed);
+      const int a16 = dv >= 0 ? dv : a16_env;
       const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
       if (a16 == 2 && !a.causal) {          // mixed 32x32 QK^T / 16x16 P.V (round 5)
         if (blocks8 >= 512) launch_mx<8>(a, s);

@@ -2,6 +2,7 @@
 // device, layout or alignment), output allocation stays in Python, every launch goes to the
 // current HIP stream (so torch.cuda.graph capture records it).
 #include <torch/extension.h>
+#include <atomic>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_ext.h>
@@ -40,7 +41,7 @@ long long* opt_stats(const c10::optional<at::Tensor>& t, long long images, int N
 // tile raster group of every GEMM launch (gemm_impl.h tile_of): 0 = the compiled default;
 // separate values for gated (GEGLU / SwiGLU) calls.  CASSMANTLE_GEMM_RASTER="G" or "G,Ggated",
 // or gemm_set_raster at run time (A/B knob)
-static int g_raster[2] = {-1, -1};
+static std::atomic<int> g_raster[2] = {{-1}, {-1}};   // read by every GEMM launch thread
 static void raster_from_env() {
   static const bool once = [] {
     const char* e = getenv("CASSMANTLE_GEMM_RASTER");
@@ -50,21 +51,23 @@ static void raster_from_env() {
     } else {
       b = 0;
     }
-    if (g_raster[0] < 0) g_raster[0] = a;
-    if (g_raster[1] < 0) g_raster[1] = b;
+    int expect = -1;
+    g_raster[0].compare_exchange_strong(expect, a);
+    expect = -1;
+    g_raster[1].compare_exchange_strong(expect, b);
     return true;
   }();
   (void)once;
 }
 void gemm_set_raster(int64_t plain, int64_t gated) {
   raster_from_env();
-  g_raster[0] = (int)plain;
-  g_raster[1] = (int)gated;
+  g_raster[0].store((int)plain);
+  g_raster[1].store((int)gated);
 }
 
 void run_gemm(GemmArgs& p, const at::Tensor& like) {
   raster_from_env();
-  p.raster = g_raster[(p.act == 4 || p.act == 6) ? 1 : 0];   // gated: GEGLU (4) / SwiGLU (6)
+  p.raster = g_raster[(p.act == 4 || p.act == 6) ? 1 : 0].load(std::memory_order_relaxed);   // gated: GEGLU (4) / SwiGLU (6)
   // output statistics are fused into the LDS-staged bf16 epilogue; shapes that take another
   // path (fp32 out, GEMV rows, batched, gated) get a separate per-channel statistics pass over
   // the output; split-K shapes accumulate them in the reduce pass
