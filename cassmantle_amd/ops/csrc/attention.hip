@@ -1396,7 +1396,11 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
         if (blocks8 >= 512) launch_mx<8>(a, s);
         else launch_mx<4>(a, s);
       } else if (a16 && !a.causal) {
-        if (blocks8 >= 512) launch_a16<8>(a, s);
+        // 8-wave blocks from 256 of them: the 4-wave build takes 130 registers (3 waves per SIMD),
+        // and at batch 1 (B = 2, 256 eight-wave blocks) the 8-wave block is 10 % faster
+        // (profiles/r5_attn_d40_nw8_batch1_ab.txt).  CASSMANTLE_ATTN16_NW8_MIN overrides (A/B knob)
+        static const int nw8_min = [] { const char* e = getenv("CASSMANTLE_ATTN16_NW8_MIN"); return e ? atoi(e) : 256; }();
+        if (blocks8 >= nw8_min) launch_a16<8>(a, s);
         else launch_a16<4>(a, s);
       } else {
         launch_nw<48, 64>(a, s);
