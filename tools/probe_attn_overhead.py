@@ -22,6 +22,8 @@ CASES = [  # name, B, Nq, H, d, fp8
     ("sd15_l3_b8", 8, 256, 8, 160, False),
     ("sd15_l2_b8", 8, 1024, 8, 80, False),
     ("sd15_l1_b2", 2, 4096, 8, 40, False),
+    ("sd15_l3_b2", 2, 256, 8, 160, False),
+    ("sd15_l2_b2", 2, 1024, 8, 80, False),
 ]
 
 
