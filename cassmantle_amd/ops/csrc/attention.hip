@@ -986,8 +986,14 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
   // CASSMANTLE_ATTN_NW=4: never the 8-wave block (A/B knob: two 4-wave blocks per CU are not
   // lock-stepped by one block's per-tile barrier, at twice the K/V tile loads)
   static const int nw_cap = [] { const char* e = getenv("CASSMANTLE_ATTN_NW"); return e ? atoi(e) : 8; }();
+  // 4-wave blocks from 512 of them, or -- UNet-sized sequences (>= 256 queries) -- from 16: at
+  // batch 1 (levels 2 / 3 of SD-1.5: 128 / 32 four-wave blocks) the 4-wave block shares each K/V
+  // tile over twice the queries and ran 9-15 % faster than twice as many 2-wave blocks
+  // (profiles/r5_attn_nw4_batch1_ab.txt); text-encoder / scorer shapes keep the 512 rule.
+  // CASSMANTLE_ATTN_NW4_MIN overrides the 16 (A/B knob)
+  static const int nw4_min = [] { const char* e = getenv("CASSMANTLE_ATTN_NW4_MIN"); return e ? atoi(e) : 16; }();
   if (DO <= 96 && blocks8 >= 1024 && nw_cap >= 8) launch_t<DQK, DO, 8>(a, s);   // 8 waves share each K/V tile
-  else if (blocks4 >= 512) launch_t<DQK, DO, 4>(a, s);
+  else if (blocks4 >= 512 || (a.Nq >= 256 && blocks4 >= nw4_min)) launch_t<DQK, DO, 4>(a, s);
   else launch_t<DQK, DO, 2>(a, s);
 }
 
