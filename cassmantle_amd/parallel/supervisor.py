@@ -550,6 +550,8 @@ class GroupSupervisor:
             if crashed or stale or time.time() > t_end:
                 break
             time.sleep(0.05)
+        if stale and not crashed:
+            stale = self._confirm_stale(g, stale)
         culprits = sorted(set(crashed) | set(stale))
         if not culprits and suspects is not None:
             culprits = sorted(r for r in suspects if g.procs[r].exitcode is None)
@@ -559,6 +561,21 @@ class GroupSupervisor:
                 culprits = []
         codes = {r: g.procs[r].exitcode for r in range(g.world)}
         return GroupFailure(f"{reason}; exit codes {codes}", culprits)
+
+    def _confirm_stale(self, g: "_Group", stale: Sequence[int]) -> List[int]:
+        """Every live worker silent at once is more likely a host stall (CPU starvation, a
+        paused container) than that many wedged GPUs: give the heartbeats a few periods to
+        resume and keep only the workers that stay silent."""
+        live = [r for r in range(g.world) if g.procs[r].exitcode is None]
+        if len(live) < 2 or set(stale) < set(live):
+            return list(stale)
+        t_end = time.time() + max(2.0, 6 * self.heartbeat_s)
+        while time.time() < t_end:
+            time.sleep(0.1)
+            still = g.stale(self.stale_s)
+            if set(still) < set(stale):
+                return still
+        return g.stale(self.stale_s)
 
     # ------------------------------------------------------------------ lockstep rounds
     def _run_round(self, jobs) -> Dict[Tuple[str, int], np.ndarray]:
@@ -579,7 +596,7 @@ class GroupSupervisor:
                 continue
             if g.dead():
                 raise self._diagnose(g, rid, "worker exited")
-            if g.stale(self.stale_s):
+            if g.stale(self.stale_s) and self._confirm_stale(g, g.stale(self.stale_s)):
                 raise self._diagnose(g, rid, "worker stopped heart-beating", grace_s=0.0)
             if self.round_timeout > 0 and time.monotonic() - t0 > self.round_timeout:
                 raise self._diagnose(g, rid, f"round {rid} exceeded {self.round_timeout:.0f} s", grace_s=0.0)
@@ -770,7 +787,7 @@ class GroupSupervisor:
                 if g.dead():
                     failure = self._diagnose(g, max(b[0] for b in busy.values()), "worker exited",
                                              suspects=[w for w in busy if g.procs[w].exitcode is not None])
-                elif g.stale(self.stale_s):
+                elif g.stale(self.stale_s) and self._confirm_stale(g, g.stale(self.stale_s)):
                     failure = self._diagnose(g, 0, "worker stopped heart-beating", grace_s=0.0, suspects=[])
             if failure is not None:
                 for _, spans, _, _ in busy.values():

@@ -254,3 +254,31 @@ def test_weighted_ownership_and_slow_worker_does_not_hold_fast_rooms():
     assert max(done_at[r] for r in fast_rooms) < 2.0 < min(done_at[r] for r in slow_rooms), done_at
     assert fast_rounds >= 3 and slow_wall >= 3.0, (fast_rounds, slow_wall)
     assert st["dispatch"] == "async" and st["worker_rounds"]["cpu:1"] > st["worker_rounds"]["cpu:0"], st
+
+
+def test_all_workers_stale_at_once_is_a_host_stall_not_a_wedge():
+    """Every heartbeat silent together (CPU starvation under load) must not retire the whole
+    group: heartbeats that resume within the confirmation window clear their workers."""
+    import threading
+    import time
+    from types import SimpleNamespace
+
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor, _Group
+    now = time.time()
+    hb = [now - 20.0] * 3
+    g = SimpleNamespace(world=3, hb=hb, procs=[SimpleNamespace(exitcode=None)] * 3)
+    g.stale = lambda s: _Group.stale(g, s)
+    sup = SimpleNamespace(stale_s=10.0, heartbeat_s=0.1)
+
+    def resume():
+        time.sleep(0.3)
+        hb[0] = hb[2] = time.time()           # worker 1 stays silent: a real wedge
+    threading.Thread(target=resume).start()
+    assert GroupSupervisor._confirm_stale(sup, g, [0, 1, 2]) == [1]
+    # a strict subset is evidence as it stands; all silent for the whole window stays all
+    assert GroupSupervisor._confirm_stale(sup, g, [1]) == [1]
+    hb[:] = [time.time() - 20.0] * 3
+    sup.heartbeat_s = 0.01
+    t0 = time.time()
+    assert GroupSupervisor._confirm_stale(sup, g, [0, 1, 2]) == [0, 1, 2]
+    assert time.time() - t0 >= 1.9
