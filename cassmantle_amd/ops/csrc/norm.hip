@@ -587,7 +587,12 @@ static void launch_apply(const uint16_t* x, const uint16_t* x2, const long long*
   const long long step = (long long)U * g.R;                       // rows per block iteration
   long long rpb;
   if (GN_APPLY_GEOM) {
-    const long long per_img = (GN_APPLY_BLOCKS + B - 1) / B;
+    // tensors of >= CASSMANTLE_GN_BIG_MB MiB may take CASSMANTLE_GN_BIG_BLOCKS blocks (A/B knob)
+    static const int big_mb = [] { const char* e = getenv("CASSMANTLE_GN_BIG_MB"); return e ? atoi(e) : 0; }();
+    static const int big_blocks = [] { const char* e = getenv("CASSMANTLE_GN_BIG_BLOCKS"); return e ? atoi(e) : GN_APPLY_BLOCKS; }();
+    const bool big = big_mb > 0 && (long long)B * S * C * 2 >= ((long long)big_mb << 20);
+    const long long blocks = big ? big_blocks : GN_APPLY_BLOCKS;
+    const long long per_img = (blocks + B - 1) / B;
     const long long want = (S + per_img - 1) / per_img;
     rpb = step * ((want + step - 1) / step);
   } else {

@@ -23,14 +23,17 @@ GN_SHAPES = [(8, 64, 64, 320), (8, 64, 64, 640), (8, 64, 64, 960), (8, 32, 32, 6
              (8, 16, 16, 1280), (8, 16, 16, 2560), (8, 8, 8, 2560)]
 # SD-1.5 convolutions that split K (batch 4 x CFG): NHWC input, Cin -> Cout, 3x3
 CONV_SHAPES = [(8, 16, 16, 1280, 1280), (8, 16, 16, 2560, 1280), (8, 8, 8, 1280, 1280), (8, 8, 8, 2560, 1280)]
+# SDXL (batch 1 x CFG) GroupNorm applies: 128^2 / 64^2 / 32^2 levels incl. the up-block concat widths
+SDXL_GN_SHAPES = [(2, 128, 128, 320), (2, 128, 128, 640), (2, 128, 128, 960), (2, 64, 64, 640),
+                  (2, 64, 64, 1280), (2, 64, 64, 1920), (2, 32, 32, 1280), (2, 32, 32, 2560)]
 ITERS = 30
 
 
-def run(gn_only: bool = False):
+def run(gn_only: bool = False, shapes=GN_SHAPES):
     import torch
     from cassmantle_amd import ops
     from cassmantle_amd.ops._ext import ext
-    for shape in GN_SHAPES:
+    for shape in shapes:
         x = (torch.randn(*shape, device="cuda") + 0.3).to(torch.bfloat16)
         C = shape[-1]
         st = ops.new_stats(shape[0], C, "cuda")
@@ -94,8 +97,9 @@ if __name__ == "__main__":
     ap.add_argument("--trace", default=None, help="rocprofv3 kernel trace of a previous run")
     ap.add_argument("--lines", default=None, help="that run's JSON output (for --trace)")
     ap.add_argument("--gn-only", action="store_true", help="only the GroupNorm applies")
+    ap.add_argument("--sdxl", action="store_true", help="the SDXL GroupNorm shapes (implies --gn-only)")
     a = ap.parse_args()
     if a.trace:
         from_trace(a.trace, [json.loads(x) for x in open(a.lines) if x.startswith("{")])
     else:
-        run(a.gn_only)
+        run(a.gn_only or a.sdxl, SDXL_GN_SHAPES if a.sdxl else GN_SHAPES)
