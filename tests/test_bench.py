@@ -78,3 +78,26 @@ def test_bench_oversubscribe_forces_gloo_and_refuses_nccl():
     r = _run(["--gpus", "2", "--oversubscribe", "--model", "tiny", "--steps", "1", "--warmup", "0", "--no-score"],
              env_extra={"CASSMANTLE_DIST_BACKEND": "nccl"}, timeout=120)
     assert r.returncode == 2 and "refused" in r.stderr
+
+
+def test_bench_under_torchrun_four_ranks():
+    """The driver's multi-GPU launch shape (torch.distributed.run, 127.0.0.1 rendezvous, one rank
+    per device, bench.py reading RANK / WORLD_SIZE from the env): 4 gloo ranks on the CPU, one
+    JSON line from rank 0 with the whole-job aggregate."""
+    from cassmantle_amd.parallel.supervisor import free_port
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "4", "--model", "tiny", "--steps", "1", "--warmup", "1", "--no-score"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 4 and out["steps"] == 1 and out["warmup"] == 1
+    assert out["comm"]["world_size"] == 4 and out["comm"]["backend"] == "gloo"
+    assert out["config"]["parallelism"] == "dp4 (rooms)" and out["config"]["global_batch"] == 16
+    assert [p["rank"] for p in out["per_rank"]] == [0, 1, 2, 3]
+    assert abs(out["value"] - 16 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.01
