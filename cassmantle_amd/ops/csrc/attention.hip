@@ -1094,7 +1094,10 @@ typedef __attribute__((ext_vector_type(8))) int i32x8_t;
   F8_GSLOT(0, ST, kr0, vr0) F8_GSLOT(1, ST, kr1, vr1) F8_GSLOT(2, ST, kr2, vr2) F8_GSLOT(3, ST, kr3, vr3)
 #define F8_LSTORE() F8_LSLOT(0, kr0, vr0) F8_LSLOT(1, kr1, vr1) F8_LSLOT(2, kr2, vr2) F8_LSLOT(3, kr3, vr3)
 
-template <int NQ, int NS>
+// DB: two LDS stages.  The next step's K/V (already in registers) go to the other stage right
+// after this step's MFMAs, so a step ends with ONE barrier instead of barrier + store + barrier
+// (the stage written in step st was last read in step st - 1, which every wave has left).
+template <int NQ, int NS, bool DB>
 __global__ void __launch_bounds__(64 * NQ * NS, (NQ * NS >= 4) ? 8 / (NQ * NS) > 0 ? 8 / (NQ * NS) : 1 : 2)
 attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, const uint8_t* __restrict__ V8t) {
   constexpr int NWV = NQ * NS;
@@ -1104,10 +1107,11 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
   constexpr int STAGE_B = 2 * NS * TILE_B;
   constexpr int MREC = 34;               // merge record per lane: 32 O registers, m, l
   constexpr int MERGE_B = (NS - 1) * NQ * 64 * MREC * 4;
-  constexpr int LDS_B = STAGE_B > MERGE_B ? STAGE_B : MERGE_B;
+  constexpr int STAGES_B = (DB ? 2 : 1) * STAGE_B;
+  constexpr int LDS_B = STAGES_B > MERGE_B ? STAGES_B : MERGE_B;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_B];
-  uint8_t* const Ks = lds;
-  uint8_t* const Vs = lds + NS * TILE_B;
+  uint8_t* Ks = lds;                       // the stage F8_LSTORE writes
+  uint8_t* Vs = lds + NS * TILE_B;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qg = wave % NQ, ks = wave / NQ;
@@ -1168,12 +1172,12 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
   for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
   const i32x8_t ones8 = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
                          0x38383838, 0x38383838, 0x38383838, 0x38383838};   // e4m3 1.0
-  const uint8_t* const Kw = Ks + ks * TILE_B;
-  const uint8_t* const Vw = Vs + ks * TILE_B;
-
   for (int st = 0; st < nsteps; ++st) {
     const bool more = st + 1 < nsteps;
     if (more) { F8_GLOAD(st + 1) }
+    const int cur = DB ? (st & 1) * STAGE_B : 0;   // the stage this step reads
+    const uint8_t* const Kw = lds + cur + ks * TILE_B;
+    const uint8_t* const Vw = lds + cur + NS * TILE_B + ks * TILE_B;
     const int t = st * NS + ks;
     if (t < ntiles) {                      // wave-uniform: the last step may not reach every split
       f32x16_t sacc[2];
@@ -1262,10 +1266,19 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
       if constexpr (ONES)
         lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pf, lsum, 0, 0, 0, 127, 0, 127);
     }
-    __syncthreads();
-    if (more) {
-      F8_LSTORE()
+    if constexpr (DB) {
+      if (more) {
+        Ks = lds + (cur ^ STAGE_B);
+        Vs = Ks + NS * TILE_B;
+        F8_LSTORE()
+      }
       __syncthreads();
+    } else {
+      __syncthreads();
+      if (more) {
+        F8_LSTORE()
+        __syncthreads();
+      }
     }
   }
   if constexpr (ONES) l_run = lsum[0];
@@ -1332,7 +1345,14 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
 template <int NQ, int NS>
 void launch_fp8_t(const AttnArgs& a, int Hk, int Nkp, const uint8_t* K8, const uint8_t* V8t, hipStream_t s) {
   const int nqb = (a.Nq + 32 * NQ - 1) / (32 * NQ);
-  hipLaunchKernelGGL((attn_fp8_kernel<NQ, NS>), dim3(nqb * a.H * a.B), dim3(64 * NQ * NS), 0, s, a, Hk, Nkp, K8, V8t);
+  // two LDS stages on the 2-split blocks unless CASSMANTLE_FP8_DBUF=0 (A/B knob; =2 forces every
+  // variant).  Same box (profiles/r5_fp8_attn_dbuf_ab.txt): 2x2 self-attention 1.0-1.6 % faster,
+  // 4x2 3-5 %; the one-step cross-attention blocks (NS 1) +1 %, the 80 KB 1x4 stages 12-30 % slower
+  static const int dbuf = [] { const char* e = getenv("CASSMANTLE_FP8_DBUF"); return e ? atoi(e) : 1; }();
+  if (dbuf == 2 || (dbuf == 1 && NS == 2))
+    hipLaunchKernelGGL((attn_fp8_kernel<NQ, NS, true>), dim3(nqb * a.H * a.B), dim3(64 * NQ * NS), 0, s, a, Hk, Nkp, K8, V8t);
+  else
+    hipLaunchKernelGGL((attn_fp8_kernel<NQ, NS, false>), dim3(nqb * a.H * a.B), dim3(64 * NQ * NS), 0, s, a, Hk, Nkp, K8, V8t);
 }
 
 }  // namespace
