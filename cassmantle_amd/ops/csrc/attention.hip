@@ -1012,6 +1012,9 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
 // other operand, so only the P <-> V^T correspondence has to be fixed: slot 32h + j of a key
 // block holds key kappa(h, j) = 32(j>>4) + (j&3) + 8((j&15)>>2) + 4h, the key of S accumulator
 // register j&15 of key-half j>>4 in lane half h.
+#ifndef F8_VEARLY
+#define F8_VEARLY 1
+#endif
 constexpr int F8_KSTR = 80;   // LDS row stride (bytes) of the 64-byte fp8 rows: 16-lane groups
                               // of ds_read_b128 hit disjoint banks (20 r mod 64 distinct)
 
@@ -1191,6 +1194,17 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
         const i32x8_t kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
         sacc[hf] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, sacc[hf], 0, 0, 0, 127, 0, 127);
       }
+      // V fragments of this tile issued now (F8_VEARLY): their LDS latency hides behind the softmax
+      i32x8_t vfe[2];
+      if constexpr (F8_VEARLY) {
+#pragma unroll
+        for (int dc = 0; dc < 2; ++dc) {
+          const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
+          const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
+          const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
+          vfe[dc] = i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+        }
+      }
       const int kbase = t * KT;
       const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
       if (need_mask) {
@@ -1257,10 +1271,15 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
           pf[4 * hf + c] = (int)f8x4(sacc[hf][4 * c], sacc[hf][4 * c + 1], sacc[hf][4 * c + 2], sacc[hf][4 * c + 3]);
 #pragma unroll
       for (int dc = 0; dc < 2; ++dc) {
-        const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
-        const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
-        const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
-        const i32x8_t vf = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+        i32x8_t vf;
+        if constexpr (F8_VEARLY) {
+          vf = vfe[dc];
+        } else {
+          const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
+          const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
+          const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
+          vf = i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+        }
         oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
       }
       if constexpr (ONES)
