@@ -1221,7 +1221,12 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[hf][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr (ATTN_PERMLANE) {    // cross-half max by v_permlane32_swap, not ds_bpermute
+        const float2 hm = both_halves(mx);
+        mx = fmaxf(hm.x, hm.y);
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      }
       if (__builtin_expect(st == 0 || !__all(mx <= RESCALE_THR), 0)) {
         // a real branch: without the volatile asm hipcc if-converts this block and rescales O
         // and S by alpha = 1 on EVERY tile (a v_pk_mul per two O registers per tile)
@@ -1259,7 +1264,12 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
             sacc[hf][r] = pv;
             rs += pv;
           }
-        rs += __shfl_xor(rs, 32, 64);
+        if constexpr (ATTN_PERMLANE) {
+          const float2 hs = both_halves(rs);
+          rs = hs.x + hs.y;
+        } else {
+          rs += __shfl_xor(rs, 32, 64);
+        }
         l_run += rs;
       }
       // P^T fragment: element j = sacc[j >> 4][j & 15]
