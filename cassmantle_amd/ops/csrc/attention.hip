@@ -33,6 +33,9 @@ constexpr int KT = 64;  // keys per tile
 // (profiles/r4_attn_switches_ab.txt): the permlane cross-half max/sum and the static priority
 // of the younger half are 1-4 % faster and on; branch-free staging loads (value selects) were
 // 4-12 % SLOWER (their selects are VALU, the contended pipe of this kernel) and are off
+#ifndef ATTN_KBATCH
+#define ATTN_KBATCH 1
+#endif
 #ifndef ATTN_PERMLANE
 #define ATTN_PERMLANE 1
 #endif
@@ -245,10 +248,23 @@ __global__ void __launch_bounds__(64 * NW, NW >= 4 ? 8 / NW : (DO >= 128 ? 1 : 2
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[hf][r] = MF ? 0.f : -m_run;   // S - m folded into the MFMA
       const uint16_t* krow = Ks + bo + (hf * 32 + ql) * G::KSTR + 8 * hlf;
+      if constexpr (ATTN_KBATCH && NKS <= 5) {
+        // all NKS K fragments of this half in flight before its MFMA chain: hipcc otherwise
+        // issues read, wait, MFMA per k-step and every MFMA waits out a full LDS latency
+        // (ATTN_KBATCH=0: the per-step form, A/B knob)
+        // (d <= 80 only: the d = 160 blocks sit at 250 VGPRs and spill with the extra fragments)
+        bf16x8_t kf[NKS];
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
-        sacc[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sacc[hf], 0, 0, 0);
+        for (int ks = 0; ks < NKS; ++ks) kf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
+        __builtin_amdgcn_sched_barrier(0);   // (the scheduler would sink each read to its MFMA)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) sacc[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], sacc[hf], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 16));
+          sacc[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sacc[hf], 0, 0, 0);
+        }
       }
     }
 
