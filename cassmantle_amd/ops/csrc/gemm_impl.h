@@ -769,6 +769,9 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j) af2[ks][j] = as_bf16x8(Bs[a_rd[ks] + 16 * 8 * j]);
     }
+    // (without this the scheduler sinks the second step's reads below the first step's MFMAs:
+    // the round-5 A/B of this path, profiles/r5_frag_prefetch_ab.txt, compiled to the old order)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       __builtin_amdgcn_s_setprio(1);
