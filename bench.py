@@ -14,16 +14,33 @@ step time and device time of its gather (µs).
 Rank 0 also measures the streaming guess scorer (BASELINE config 1/5): MiniLM-L6 embed +
 cosine for a 64-player micro-batch, p50 latency in ms (reported as ``p50_score_ms``).
 
+After the headline timed region (its fields unchanged), a 1-GPU run also records BASELINE
+configs 4 and 5 (skippable): ``sdxl_fp8_s_per_image`` (SDXL-base 1024², 30 Euler steps, batch 1,
+fp8 attention; one warm-up + 2 timed generations, prompt -> host uint8, with its own ``finite``)
+and a short in-process live round (``live_images_per_s``, ``live_score_p50_ms`` /
+``live_score_p99_ms``: 64 simulated players scoring while the same pipeline draws 4-image rooms
+back to back, ``runtime/live.py``).
+
+Failure handling (a first multi-GPU run must end with a diagnosable record, not a silent hang):
+the launcher counts GPUs without touching HIP (visibility variables, KFD sysfs topology); the
+process-group init and every blocking collective of a rank are bounded by ``--comm-timeout-s``
+(a watchdog thread ends the rank with an error record); the launcher has an overall
+``--deadline-s``.  On a failure ONE JSON line is printed (by the launcher, or by rank 0 under
+torchrun) with ``value`` null, ``error`` and, for a collective / init failure, ``comm.error``.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4] [--baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
+import threading
 import time
+import traceback
 
 BASELINE_IMAGES_PER_SEC = None  # BASELINE.json "published": {} — no reference number
 METRICS = {"sd15": "SD-1.5 512^2 50-step images/sec (whole node) + p50 guess-score latency",
@@ -46,6 +63,13 @@ def parse():
     p.add_argument("--overlap", action="store_true", help="VAE decode on a side stream, overlapped with the next step's denoise")
     p.add_argument("--no-batch1", action="store_true", help="skip the batch-1 latency (s/image one room waits)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--no-sdxl", action="store_true", help="skip the SDXL fp8 extra (BASELINE config 4)")
+    p.add_argument("--no-live", action="store_true", help="skip the in-process live-round extra (config 5)")
+    p.add_argument("--live-seconds", type=float, default=8.0)
+    p.add_argument("--live-players", type=int, default=64)
+    p.add_argument("--comm-timeout-s", type=float, default=180.0,
+                   help="bound on the process-group init and on every blocking collective of a rank")
+    p.add_argument("--deadline-s", type=float, default=1500.0, help="launcher: overall deadline of the job")
     p.add_argument("--oversubscribe", action="store_true",
                    help="allow --gpus N above the visible GPU count: the N ranks share the GPUs "
                         "(rank r on GPU r mod visible) over gloo with a host gather; RCCL refuses "
@@ -122,28 +146,120 @@ def scorer_bench(device) -> dict:
 
 
 def _visible_gpus() -> int:
-    """Device count WITHOUT initialising the GPU (on this ROCm image ``device_count`` does not
-    create a HIP context, so the launcher may still start fresh rank processes afterwards)."""
-    import torch
-    return torch.cuda.device_count()
+    """GPU count WITHOUT any HIP call (the launcher starts fresh rank processes afterwards and
+    must never initialise the GPU itself; ``torch.cuda.device_count`` may fall back to a HIP
+    runtime init when amdsmi is unavailable).  A visibility variable wins; otherwise the GPU
+    nodes of the KFD topology (``simd_count`` > 0; CPU nodes report 0) are counted."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    n = 0
+    for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(prop) as f:
+                kv = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+            n += int(kv.get("simd_count", "0")) > 0
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def _config_of(args, world: int) -> dict:
+    return {"model": args.model, "global_batch": world * args.batch, "parallelism": f"dp{world} (rooms)"}
+
+
+def error_record(args, world: int, error: str, comm_error: str = None, backend: str = None) -> dict:
+    """The one JSON line of a failed job: the headline keys with ``value`` null."""
+    out = {"metric": METRICS.get(args.model, f"{args.model} images/sec"), "value": None, "unit": "images/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (seeds.txt template prompts, random-init weights)",
+           "config": _config_of(args, world), "error": error}
+    if comm_error is not None:
+        out["comm"] = {"backend": backend, "world_size": world, "error": comm_error}
+    return out
+
+
+class RankFailure(Exception):
+    def __init__(self, kind: str, msg: str) -> None:
+        super().__init__(msg)
+        self.kind = kind                    # "comm-init" | "comm" | "rank"
+
+
+def report_failure(args, rank: int, world: int, kind: str, msg: str, backend: str = None) -> None:
+    """Launched by our launcher: a per-rank record for it to relay.  Under torchrun: rank 0
+    prints the job's one JSON line itself."""
+    rec = {"rank": rank, "kind": kind, "error": msg[-2000:], "backend": backend}
+    errdir = os.environ.get("CASSMANTLE_BENCH_ERRDIR")
+    if errdir:
+        try:
+            with open(os.path.join(errdir, f"rank{rank}.json"), "w") as f:
+                json.dump(rec, f)
+        except OSError:
+            pass
+    elif rank == 0:
+        comm = msg if kind.startswith("comm") else None
+        print(json.dumps(error_record(args, world, f"rank 0 {kind}: {msg[-500:]}", comm, backend)), flush=True)
+    print(f"[bench] rank {rank} failed ({kind}): {msg[-2000:]}", file=sys.stderr, flush=True)
+
+
+class Watchdog:
+    """Bounds the blocking phases of a rank: ``arm(stage, s)`` before a process-group init or a
+    blocking collective / device sync behind collectives, ``disarm()`` after.  A stage still
+    armed at its deadline (a dead or wedged peer: RCCL would wait forever) ends THIS process
+    with a failure record (``os._exit``: the main thread is stuck inside the runtime)."""
+
+    def __init__(self, args, rank: int, world: int) -> None:
+        self.args, self.rank, self.world = args, rank, world
+        self.backend = None
+        self._stage, self._deadline = None, None
+        self._mu = threading.Lock()
+        threading.Thread(target=self._run, name="bench-watchdog", daemon=True).start()
+
+    def arm(self, stage: str, seconds: float) -> None:
+        with self._mu:
+            self._stage, self._deadline = stage, time.monotonic() + seconds
+
+    def disarm(self) -> None:
+        with self._mu:
+            self._stage, self._deadline = None, None
+
+    def _run(self) -> None:
+        while True:
+            time.sleep(0.25)
+            with self._mu:
+                stage, dl = self._stage, self._deadline
+            if dl is not None and time.monotonic() > dl:
+                kind = "comm-init" if stage == "comm-init" else "comm"
+                report_failure(self.args, self.rank, self.world, kind,
+                               f"{stage} did not finish within its bound (a peer rank died or hung)", self.backend)
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(3)
 
 
 def launch_ranks(args) -> int:
     """``bench.py --gpus N`` with no torchrun environment: start N fresh rank processes (one per
     GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; RCCL on GPUs, gloo on the CPU) before
     this process makes any GPU call, relay rank 0's JSON line and fail if any rank fails.
-    Every rank's stdout/stderr is inherited; only rank 0 prints the result line."""
+    Every rank's stdout/stderr is inherited; rank 0 prints the result line.  On a failure (a
+    rank exits non-zero, or the job passes ``--deadline-s``) the other ranks are stopped within
+    seconds and THIS process prints the job's one JSON line with the ranks' failure records."""
     import signal
     import socket
     import subprocess
+    import tempfile
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    errdir = tempfile.mkdtemp(prefix="cassmantle-bench-")
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   CASSMANTLE_BENCH_ERRDIR=errdir)
         if args.oversubscribe:
             env["CASSMANTLE_DIST_BACKEND"] = "gloo"
         # host threads per rank (torchrun's default is 1): N ranks must not each spin up a
@@ -151,6 +267,8 @@ def launch_ranks(args) -> int:
         env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc = 0
+    why = None
+    t_end = time.monotonic() + args.deadline_s
     try:
         live = list(procs)
         while live:
@@ -161,16 +279,43 @@ def launch_ranks(args) -> int:
                 live.remove(p)
                 if code != 0 and rc == 0:
                     rc = code if code > 0 else 1
-                    print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks",
-                          file=sys.stderr, flush=True)
+                    why = f"rank {procs.index(p)} exited with {code}"
+                    print(f"[bench] {why}; stopping the other ranks", file=sys.stderr, flush=True)
                     for q in live:           # peers would block in a collective forever
                         q.send_signal(signal.SIGTERM)
+                    t_end = min(t_end, time.monotonic() + 10.0)
+            if live and time.monotonic() > t_end:
+                if rc == 0:
+                    rc = 124
+                    why = f"job exceeded the launcher deadline of {args.deadline_s:.0f} s"
+                    print(f"[bench] {why}; killing the ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    q.kill()
+                break
             time.sleep(0.2)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+    if rc != 0:
+        recs = []
+        for f in sorted(glob.glob(os.path.join(errdir, "rank*.json"))):
+            try:
+                with open(f) as fh:
+                    recs.append(json.load(fh))
+            except (OSError, ValueError):
+                pass
+        comm = [r for r in recs if str(r.get("kind", "")).startswith("comm")]
+        backend = next((r.get("backend") for r in recs if r.get("backend")), None)
+        detail = "; ".join(f"rank {r['rank']} {r['kind']}: {r['error'][-300:]}" for r in recs)
+        out = error_record(args, args.gpus, why + (f" ({detail})" if detail else ""),
+                           "; ".join(f"rank {r['rank']}: {r['error'][-300:]}" for r in comm) if comm
+                           else (why if rc == 124 else None), backend)
+        print(json.dumps(out), flush=True)
+    for f in glob.glob(os.path.join(errdir, "*")):
+        os.remove(f)
+    os.rmdir(errdir)
     return rc
 
 
@@ -196,8 +341,29 @@ def main() -> int:
     if env_world is None and args.gpus < 1:
         print("[bench] --gpus must be >= 1", file=sys.stderr)
         return 2
+    if (os.environ.get("CASSMANTLE_DIAG_TWICE", "0") == "1"
+            and os.environ.get("CASSMANTLE_DIAG_TWICE_ACK") != "wrong-results"):
+        # (tools/diag_twice.py traces set the acknowledgement; a record of such a run is invalid)
+        print("[bench] CASSMANTLE_DIAG_TWICE=1 (a timing diagnostic with WRONG results) refused", file=sys.stderr)
+        return 2
     if args.baseline:
         os.environ["CASSMANTLE_OPS"] = "torch"
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    wd = Watchdog(args, rank, world)
+    try:
+        return run_rank(args, wd)
+    except RankFailure as e:
+        report_failure(args, rank, world, e.kind, str(e), wd.backend)
+    except BaseException as e:  # noqa: BLE001 - one record, then a non-zero exit
+        report_failure(args, rank, world, "rank", "".join(traceback.format_exception(type(e), e, e.__traceback__)),
+                       wd.backend)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(3)          # no collective teardown: a peer may be gone
+
+
+def run_rank(args, wd: "Watchdog") -> int:
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -207,9 +373,17 @@ def main() -> int:
     from cassmantle_amd.pipeline import SPECS, StableDiffusion
     from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
 
-    ctx = cdist.init_from_env()
+    wd.backend = os.environ.get("CASSMANTLE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    wd.arm("comm-init", args.comm_timeout_s)
+    try:
+        ctx = cdist.init_from_env(timeout_s=args.comm_timeout_s)
+    except Exception as e:  # noqa: BLE001
+        raise RankFailure("comm-init", f"{type(e).__name__}: {e}") from e
+    wd.disarm()
     rank, world = ctx.rank, ctx.world_size
     device = ctx.device
+    if world > 1:
+        wd.backend = dist.get_backend()
     if args.baseline:
         ops.set_mode("torch")
     torch.manual_seed(0)
@@ -268,6 +442,9 @@ def main() -> int:
             gather_ms.append((e0, e1))
         return img
 
+    # the warm-up (graph capture) and timed steps enqueue C2 gathers that wait for the peers:
+    # every host wait behind them is bounded (a dead peer would block RCCL forever)
+    wd.arm("warm-up steps + barrier", args.comm_timeout_s + 120.0 * max(1, args.warmup))
     for w in range(args.warmup):
         one_step(w)
     torch.cuda.synchronize(device) if device.type == "cuda" else None
@@ -275,6 +452,7 @@ def main() -> int:
         dist.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
+    wd.arm("timed steps + barrier", args.comm_timeout_s + 60.0 * args.steps)
     from cassmantle_amd.utils.tracing import TRACER
     TRACER.flush()
     TRACER.reset()                      # stage means over the timed generations only
@@ -288,6 +466,7 @@ def main() -> int:
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
+    wd.arm("timing collectives", args.comm_timeout_s)
     mine = elapsed
     # finiteness of the final LATENTS of the last TIMED generation (the uint8 image is finite by
     # construction); read before the batch-1 runs below replace it
@@ -310,6 +489,7 @@ def main() -> int:
         dist.all_gather(allv, mine_t)
         per_rank = [{"rank": i, "ms_per_step": round(float(v[0]), 2), "gather_us": round(float(v[1]), 1)}
                     for i, v in enumerate(allv)]
+    wd.disarm()
     # batch-1 latency: one room's single image end to end (prompt -> uint8 on host), what a
     # serving room waits on; one warm-up generation (graph capture for batch 1), then 2 timed
     b1 = None
@@ -326,6 +506,16 @@ def main() -> int:
     score = {}
     if rank == 0 and not args.no_score:
         score = scorer_bench(device)    # noqa: F841 - reported below
+
+    # BASELINE configs 5 and 4 as extras of a 1-GPU record, after every headline measurement
+    extras = {}
+    if world == 1 and device.type == "cuda" and args.model == "sd15" and not args.baseline:
+        if not args.no_live:
+            extras.update(live_extra(args, sd, device, room_prompts, negative))
+        if not args.no_sdxl:
+            del sd
+            torch.cuda.empty_cache()
+            extras.update(sdxl_extra(device, negative))
 
 
     if rank == 0:
@@ -357,14 +547,73 @@ def main() -> int:
             "stage_overlap": sd.decode_stream is not None,
             "stage_mean_ms": stage_ms,      # device time per timed generation
             **score,
+            **extras,
         }
         if per_rank is not None:
             out["per_rank"] = per_rank
             out["comm"] = {"backend": dist.get_backend(), "world_size": world,
                            "oversubscribed": bool(args.oversubscribe)}
         print(json.dumps(out), flush=True)
+    wd.arm("shutdown barrier", args.comm_timeout_s + 300.0)
     cdist.shutdown()
+    wd.disarm()
     return 0
+
+
+def live_extra(args, sd, device, room_prompts, negative) -> dict:
+    """BASELINE config 5 (in-process, this GPU): ``--live-players`` players stream guesses through
+    the micro-batching scorer (graph-replayed MiniLM on a high-priority stream) while the
+    headline pipeline draws 4-image rooms back to back (prompt -> host uint8)."""
+    from cassmantle_amd.runtime.live import live_round_inprocess
+    from cassmantle_amd.scoring.batcher import BatchingScorer
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+    scorer = BatchingScorer(EncoderBackend(device=str(device), stream_priority=-1), 0.01, window_ms=1.0)
+
+    def gen(step: int) -> int:
+        imgs = sd.generate(room_prompts(20_000 + step), negative,
+                           [500_000 + 10 * step + j for j in range(args.batch)],
+                           steps=args.denoise_steps, scheduler=args.scheduler)
+        return len(imgs)
+    r = live_round_inprocess(gen, scorer, players=args.live_players, seconds=args.live_seconds, seed=3)
+    return {"live_images_per_s": r["images_per_s"], "live_score_p50_ms": r["load_p50_ms"],
+            "live_score_p99_ms": r["load_p99_ms"],
+            "live": {"players": r["players"], "requests": r["requests"], "seconds": r["seconds"],
+                     "generations": r["generations"], "batch_per_room": args.batch, "topology": "in-process"}}
+
+
+def sdxl_extra(device, negative) -> dict:
+    """BASELINE config 4: SDXL-base 1024², 30 Euler steps, batch 1, fp8 (OCP e4m3) UNet
+    attention on this GPU; one warm-up generation (graph capture), then 2 timed, each prompt ->
+    host uint8 (the median is reported), with the finiteness of the timed latents."""
+    import numpy as np
+    from cassmantle_amd.game.prompts import SyntheticPromptGenerator, image_prompt, load_seeds, load_styles
+    from cassmantle_amd.pipeline import SPECS, StableDiffusion
+    spec = SPECS["sdxl"]
+    t_build = time.perf_counter()
+    xl = StableDiffusion(spec, device=device, fp8_attention=True, seed=0)
+    gen = SyntheticPromptGenerator(salt=11)
+    seeds_txt, styles = load_seeds(), load_styles()
+
+    def prompt(i):
+        text = gen.generate(seeds_txt[i % len(seeds_txt)] + "\nChapter 1\n\n", True)
+        return [image_prompt(styles[i % len(styles)], text, "A {style} style piece depicting the following: ")]
+    xl.generate(prompt(0), negative, [1])
+    warm_s = time.perf_counter() - t_build
+    lat, finite = [], True
+    for i in range(2):
+        t1 = time.perf_counter()
+        try:
+            xl.generate(prompt(1 + i), negative, [2 + i])
+        except Exception as e:  # noqa: BLE001 - non-finite latents raise ImageGenerationError
+            if "non-finite" not in str(e):
+                raise
+            finite = False
+        lat.append(time.perf_counter() - t1)
+    return {"sdxl_fp8_s_per_image": round(float(np.median(lat)), 4),
+            "sdxl": {"resolution": spec.resolution, "steps": spec.steps, "scheduler": spec.scheduler,
+                     "guidance": spec.guidance, "batch": 1, "attention": "fp8 (e4m3, block-scaled MFMA)",
+                     "timed": len(lat), "s_per_image_each": [round(x, 4) for x in lat], "finite": finite,
+                     "build_and_warmup_s": round(warm_s, 1)}}
 
 
 if __name__ == "__main__":

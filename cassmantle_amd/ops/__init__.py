@@ -56,6 +56,11 @@ _tune_loaded = False
 # CASSMANTLE_DIAG_TWICE=1 launches every GEMM / conv twice back to back, so a kernel trace shows
 # each call cold (operands as the pipeline leaves them) and then warm (tools/diag_twice.py)
 _DIAG_TWICE = os.environ.get("CASSMANTLE_DIAG_TWICE", "0") == "1"
+if _DIAG_TWICE and os.environ.get("CASSMANTLE_DIAG_TWICE_ACK") != "wrong-results":
+    # never let the diagnostic reach a serving or bench process by accident
+    raise RuntimeError("CASSMANTLE_DIAG_TWICE=1 makes every GEMM / conv result WRONG (epilogue "
+                       "statistics and residuals applied twice); it is a timing diagnostic for "
+                       "tools/diag_twice.py only: also set CASSMANTLE_DIAG_TWICE_ACK=wrong-results")
 
 
 def load_gemm_tuning(path: Optional[str] = None) -> int:
@@ -689,6 +694,15 @@ def pair_cosine(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 def cosine_topk(table: torch.Tensor, vec: torch.Tensor, k: int):
     if not _use_hip(table):
         return ref.cosine_topk(table, vec, k)
+    if k > 1024:
+        # the in-tree bitonic top-k holds at most 1024 candidates per block (bindings.cpp);
+        # larger k: in-tree cosine GEMV + a stable sort, the reference ordering (ties: lower row)
+        table = table.contiguous()
+        sims = torch.empty(table.shape[0], device=table.device, dtype=torch.float32)
+        ext().cosine_gemv(table, vec.contiguous(), sims)
+        order = torch.sort(sims, descending=True, stable=True)
+        k = min(int(k), sims.shape[0])
+        return torch.return_types.topk((order.values[:k].contiguous(), order.indices[:k].contiguous()))
     # one fused in-tree pipeline (misc.hip): block-wise cosine + bitonic top-k + merge passes;
     # equal scores rank the lower row first (torch.return_types-like (values, indices))
     vals, idx = ext().cosine_topk(table.contiguous(), vec.contiguous(), int(k))

@@ -31,6 +31,23 @@ class DistContext:
         return self.rank == 0
 
 
+def _inject_init_fault(rank: int) -> None:
+    """Test hook (SURVEY §5.3 fault injection): ``CASSMANTLE_FAULT_DIST_INIT=raise|hang`` makes
+    the ranks listed in ``CASSMANTLE_FAULT_DIST_RANKS`` (comma-separated, default every rank)
+    fail or wedge at the process-group init, as a broken RCCL / xGMI setup would."""
+    mode = os.environ.get("CASSMANTLE_FAULT_DIST_INIT")
+    if not mode:
+        return
+    ranks = os.environ.get("CASSMANTLE_FAULT_DIST_RANKS")
+    if ranks and str(rank) not in ranks.split(","):
+        return
+    if mode == "raise":
+        raise RuntimeError(f"injected process-group init failure on rank {rank} (CASSMANTLE_FAULT_DIST_INIT)")
+    if mode == "hang":
+        import time
+        time.sleep(1e6)
+
+
 def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> DistContext:
     """Reads RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT (torchrun contract)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -43,6 +60,7 @@ def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> Di
     else:
         device = torch.device("cpu")
     be = None
+    _inject_init_fault(rank)
     if world > 1:
         # CASSMANTLE_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on ONE GPU
         # (RCCL refuses two ranks on a device); production is always nccl (= RCCL) on GPUs

@@ -330,7 +330,17 @@ class GroupSupervisor:
         self._probation = False
         self.probes: List[Dict[str, Any]] = []
         self._q: "queue.Queue" = queue.Queue()
-        self._wake_r, self._wake_w = pymp.Pipe(duplex=False)
+        # async dispatch waits on the worker pipes AND this self-pipe; lockstep only on ``_q``,
+        # so the self-pipe exists only in async mode.  Both ends are non-blocking and a write is
+        # skipped while a wake-up is already pending: a writer can never block on a full pipe
+        # (a blocking pipe that nobody drained hung every submit() after ~13k)
+        self._wake_r: Optional[int] = None
+        self._wake_w: Optional[int] = None
+        if dispatch == "async":
+            self._wake_r, self._wake_w = os.pipe()
+            os.set_blocking(self._wake_r, False)
+            os.set_blocking(self._wake_w, False)
+        self._wake_pending = False
         self._wake_lock = threading.Lock()
         self._closed = False
         self._ready = threading.Event()
@@ -449,11 +459,11 @@ class GroupSupervisor:
         return (self.group is None and bool(self.retired) and not self._closed and self._probe_thread is None
                 and time.time() >= self._next_probe)
 
-    def _start_probe(self) -> None:
+    def _start_probe(self, devices: Optional[Sequence[str]] = None) -> None:
         """With no live group and the back-off passed: start a fresh group on every retired
-        device on a background thread.  Requests keep failing fast meanwhile (a
-        probe must not hold a batch for a whole group start)."""
-        back = [d for d in self.all_devices if d in self.retired]
+        device (or on ``devices``) on a background thread.  Requests keep failing fast meanwhile
+        (a probe must not hold a batch for a whole group start)."""
+        back = [d for d in self.all_devices if d in self.retired and (devices is None or d in devices)]
         log.info("[INFO] re-probing retired devices %s", back)
         self._next_probe = float("inf")
         t0 = time.time()
@@ -493,15 +503,14 @@ class GroupSupervisor:
         bad = [obj.group.devices[r] for r in obj.culprits if obj.group is not None and 0 <= r < obj.group.world]
         self._probe_backoff = min(2 * self._probe_backoff, 3600.0)
         self._next_probe = time.time() + self._probe_backoff
-        if bad and len(bad) < len(back):              # the innocent devices are tried again at once
-            for d in back:
-                if d not in bad:
-                    self.retired.pop(d, None)
-            self.healthy = [d for d in self.all_devices if d not in self.retired]
-            try:
-                self._start_group()
-            except GroupFailure as e:
-                self._restart(e.culprits, str(e))
+        if bad and len(bad) < len(back) and not self._closed:
+            # the innocent devices are tried again at once, on the same background path: their
+            # group start (model load, graph capture) must not stall this loop, so
+            # requests keep failing fast until the probe's group is adopted
+            innocent = [d for d in back if d not in bad]
+            for d in innocent:
+                self.retired[d] = "re-probe pending (innocent in a failed probe)"
+            self._start_probe(innocent)
 
     def _round_ok(self) -> None:
         self.rounds += 1
@@ -511,10 +520,24 @@ class GroupSupervisor:
 
     # ------------------------------------------------------------------ requests
     def _wake(self) -> None:
+        if self._wake_w is None:                 # lockstep: the loop blocks on _q itself
+            return
         with self._wake_lock:
+            if self._wake_pending:
+                return
+            self._wake_pending = True
             try:
-                self._wake_w.send_bytes(b"w")
-            except Exception:  # noqa: BLE001
+                os.write(self._wake_w, b"w")
+            except (BlockingIOError, OSError):   # full or closed: a wake-up is already queued
+                pass
+
+    def _drain_wake(self) -> None:
+        with self._wake_lock:
+            self._wake_pending = False
+            try:
+                while os.read(self._wake_r, 4096):
+                    pass
+            except (BlockingIOError, OSError):
                 pass
 
     def submit(self, room: str, prompts: Sequence[str], seeds: Sequence[int]) -> cf.Future:
@@ -554,7 +577,10 @@ class GroupSupervisor:
             stale = self._confirm_stale(g, stale)
         culprits = sorted(set(crashed) | set(stale))
         if not culprits and suspects is not None:
-            culprits = sorted(r for r in suspects if g.procs[r].exitcode is None)
+            # async dispatch runs no collective after the start handshake, so a busy worker that
+            # reported an error, exited (even with 0 / REPORTED_EXIT) or timed out is the culprit
+            # itself, never collateral of a failed peer
+            culprits = sorted(set(suspects))
         elif not culprits and rid > 0:
             culprits = [r for r in range(g.world) if g.progress[r] < rid and g.procs[r].exitcode is None]
             if len(culprits) == g.world:         # nobody finished: no evidence against anyone
@@ -745,8 +771,7 @@ class GroupSupervisor:
             waitables = [self._wake_r] + [g.conns[w] for w in busy] if g is not None else [self._wake_r]
             ready = mp_wait(waitables, timeout)
             if self._wake_r in ready:
-                while self._wake_r.poll():
-                    self._wake_r.recv_bytes()
+                self._drain_wake()
             if g is None or not busy:
                 continue
             # ---- results and failures
@@ -849,6 +874,11 @@ class GroupSupervisor:
         if self.group is not None:
             self.group.kill()
             self._adopt(None)
+        if self._wake_w is not None and not self._thread.is_alive():
+            with self._wake_lock:                # no writer can reach a recycled fd number
+                w, r, self._wake_w = self._wake_w, self._wake_r, None
+            os.close(w)
+            os.close(r)
 
     def status(self) -> Dict[str, Any]:
         return {"epoch": self.epoch, "live_devices": self.live_devices(), "retired": dict(self.retired),

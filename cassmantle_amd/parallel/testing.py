@@ -10,8 +10,13 @@ configured through the worker environment:
   returns at once, as the real pipeline does when it only QUEUES the work, but its completion
   event never fires: a GPU wedged inside the denoise graph), ``slow`` (every generation takes
   ``CASSMANTLE_FAULT_DELAY`` seconds longer: a straggler GPU), ``start_kill`` (the worker dies
-  while its generator is being built: a fault during model load or graph capture);
-* ``CASSMANTLE_FAULT_TRIGGER``: a file; the fault fires only once it exists.
+  while its generator is being built: a fault during model load or graph capture), ``exit0``
+  (the process leaves mid-round with exit code 0: no crash signature, still the culprit);
+* ``CASSMANTLE_FAULT_TRIGGER``: a file; the fault fires only once it exists.  A ``{index}`` in
+  the path is replaced by the slot's index, so a test can arm and disarm slots one by one
+  (``CASSMANTLE_FAULT_SLOT`` may then name several slots, comma-separated);
+* ``CASSMANTLE_FAULT_START_DELAY``: every worker sleeps this long while its generator is built
+  (a slow model load / graph capture), fault or not.
 
 Every image carries the generating slot's index in its top-left 8x8 block (value
 ``40 * (index + 1)``, robust to JPEG), so a test can tell which device drew a room's round.
@@ -28,18 +33,19 @@ class StampedGenerator(SolidImageGenerator):
     def __init__(self, slot: str, res: int = 32) -> None:
         super().__init__(res)
         self.slot = slot
-        self.index = int(slot.split(":")[1]) if ":" in slot else 0
-        self.fault_slot = os.environ.get("CASSMANTLE_FAULT_SLOT")
+        self.index = _slot_index(slot)
         self.fault_mode = os.environ.get("CASSMANTLE_FAULT")
-        self.trigger = os.environ.get("CASSMANTLE_FAULT_TRIGGER")
+        self.trigger = _trigger(self.index)
 
     def _armed(self) -> bool:
-        return self.slot == self.fault_slot and bool(self.trigger) and os.path.exists(self.trigger)
+        return _faulty(self.slot) and bool(self.trigger) and os.path.exists(self.trigger)
 
     def generate(self, prompts, negative_prompt, seeds):
         if self._armed():
             if self.fault_mode == "kill":
                 os._exit(17)
+            if self.fault_mode == "exit0":       # leaves mid-round with a CLEAN exit code
+                os._exit(0)
             if self.fault_mode == "hang":
                 time.sleep(3600)
             if self.fault_mode == "fail":
@@ -79,10 +85,23 @@ class AsyncStampedGenerator(StampedGenerator):
         return DeviceImages(img, None, _Done())
 
 
+def _slot_index(slot: str) -> int:
+    return int(slot.split(":")[1].split("#")[0]) if ":" in slot else 0
+
+
+def _trigger(index: int) -> str:
+    return os.environ.get("CASSMANTLE_FAULT_TRIGGER", "").replace("{index}", str(index))
+
+
+def _faulty(slot: str) -> bool:
+    return slot in os.environ.get("CASSMANTLE_FAULT_SLOT", "").split(",")
+
+
 def stamped_generator(cfg, device: str, spec) -> StampedGenerator:
-    trig = os.environ.get("CASSMANTLE_FAULT_TRIGGER")
-    if (os.environ.get("CASSMANTLE_FAULT") == "start_kill" and (spec.slot or device) == os.environ.get("CASSMANTLE_FAULT_SLOT")
-            and trig and os.path.exists(trig)):
+    slot = spec.slot or device
+    trig = _trigger(_slot_index(slot))
+    time.sleep(float(os.environ.get("CASSMANTLE_FAULT_START_DELAY", "0")))
+    if os.environ.get("CASSMANTLE_FAULT") == "start_kill" and _faulty(slot) and trig and os.path.exists(trig):
         os._exit(17)                     # dies without reporting, before the "ready" message
     cls = AsyncStampedGenerator if os.environ.get("CASSMANTLE_FAULT") == "async_hang" else StampedGenerator
     return cls(spec.slot or device, res=cfg.model.resolution)

@@ -31,6 +31,9 @@ WS_PROTOCOL = "cassmantle_amd.api.wsproto:RFC6455Protocol"
 
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
+    if os.environ.get("CASSMANTLE_DIAG_TWICE", "0") == "1":
+        print("[serve] CASSMANTLE_DIAG_TWICE=1 (a timing diagnostic with WRONG results) refused", file=sys.stderr)
+        return 2
     ap = argparse.ArgumentParser(add_help=True)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)

@@ -1019,7 +1019,8 @@ def test_gn_linear_folds_groupnorm_into_areg(B, S, C, N):
 
 @pytest.mark.parametrize("V,D,k,dtype", [(1, 300, 1, torch.float32), (5000, 300, 51, torch.bfloat16),
                                          (100_003, 300, 64, torch.float32), (1_000_000, 300, 51, torch.bfloat16),
-                                         (70_000, 64, 1024, torch.bfloat16)])
+                                         (70_000, 64, 1024, torch.bfloat16),
+                                         (70_000, 64, 2000, torch.bfloat16)])   # k > 1024: GEMV + stable sort
 def test_cosine_topk_in_tree(V, D, k, dtype):
     """K15 (``most_similar``, reference src/backend.py:297-301): fused cosine GEMV + bitonic
     top-k + merge passes, no ATen kernel.  Exact ties (duplicated rows) rank the lower row

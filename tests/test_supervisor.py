@@ -37,6 +37,7 @@ def _cfg(rooms):
 
 
 @pytest.mark.parametrize("fault,dispatch", [("kill", "async"), ("hang", "async"), ("async_hang", "async"),
+                                            ("exit0", "async"),
                                             ("kill", "lockstep"), ("async_hang", "lockstep")])
 def test_dead_worker_retired_survivors_take_over(fault, dispatch):
     from fastapi.testclient import TestClient
@@ -282,3 +283,87 @@ def test_all_workers_stale_at_once_is_a_host_stall_not_a_wedge():
     t0 = time.time()
     assert GroupSupervisor._confirm_stale(sup, g, [0, 1, 2]) == [0, 1, 2]
     assert time.time() - t0 >= 1.9
+
+
+@pytest.mark.parametrize("dispatch", ["lockstep", "async"])
+def test_many_submits_never_block(dispatch):
+    """the wake-up self-pipe was written on every submit() but drained only by the
+    async loop; in lockstep the 64 KiB pipe filled after ~13k submissions and every later
+    submit() (and close()) blocked forever.  With no device every request fails fast, so 20k
+    submissions must all return and resolve within seconds in both dispatch modes."""
+    import threading
+    import time
+    from cassmantle_amd.game.content import ImageGenerationError
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1"]
+    sup = GroupSupervisor(_cfg(rooms), [], rooms, window_s=0.0, dispatch=dispatch)
+    futs = []
+    try:
+        assert sup.wait_ready(30)
+
+        def flood():
+            for i in range(20_000):
+                futs.append(sup.submit(rooms[i % 2], ["p"], [i]))
+        t = threading.Thread(target=flood, daemon=True)
+        t0 = time.monotonic()
+        t.start()
+        t.join(60)
+        assert not t.is_alive(), f"submit() blocked after {len(futs)} submissions"
+        for f in futs:
+            with pytest.raises(ImageGenerationError):
+                f.result(timeout=30)
+        assert time.monotonic() - t0 < 60
+    finally:
+        t_close = time.monotonic()
+        sup.close()
+        assert time.monotonic() - t_close < 30
+    assert len(futs) == 20_000
+
+
+def test_innocent_devices_of_a_failed_probe_restart_in_the_background():
+    """a re-probe that fails with a named culprit restarts the innocent devices on the
+    background probe path, not synchronously on the supervisor loop: requests keep failing fast
+    while that group starts (3 s model load here), and the innocent device serves afterwards."""
+    import time
+    from cassmantle_amd.game.content import ImageGenerationError
+    from cassmantle_amd.parallel.supervisor import GroupSupervisor
+    rooms = ["", "1"]
+    with tempfile.TemporaryDirectory() as d:
+        trig = os.path.join(d, "fault{index}")
+        for i in (0, 1):
+            open(trig.replace("{index}", str(i)), "w").close()
+        env = {"CASSMANTLE_FAULT_SLOT": "cpu:0,cpu:1", "CASSMANTLE_FAULT": "start_kill",
+               "CASSMANTLE_FAULT_TRIGGER": trig, "CASSMANTLE_FAULT_START_DELAY": "3.0"}
+        sup = GroupSupervisor(_cfg(rooms), ["cpu:0", "cpu:1"], rooms,
+                              gen_factory="cassmantle_amd.parallel.testing:stamped_generator",
+                              window_s=0.1, worker_env=env, start_timeout_s=240, reprobe_s=1.0)
+        try:
+            assert sup.wait_ready(240)
+            assert sup.live_devices() == [] and sorted(sup.retired) == ["cpu:0", "cpu:1"], sup.status()
+            os.remove(trig.replace("{index}", "0"))            # cpu:0 recovers, cpu:1 stays bad
+            t_end = time.time() + 240
+            while not sup.probes and time.time() < t_end:       # first probe: cpu:1 dies at start
+                time.sleep(0.05)
+            assert sup.probes and sup.probes[0]["ok"] is False, sup.probes
+            time.sleep(0.5)                                     # the innocent probe is starting (>= 3 s)
+            assert sup._probe_thread is not None, sup.status()
+            fast = []
+            while sup._probe_thread is not None and time.time() < t_end:
+                t0 = time.time()
+                with pytest.raises(ImageGenerationError, match="repeats"):
+                    sup.submit("", ["p"], [1]).result(timeout=60)
+                fast.append(time.time() - t0)
+                time.sleep(0.2)
+            assert fast and max(fast) < 1.5, fast              # never held by the group start
+            img = None
+            while img is None and time.time() < t_end:
+                try:
+                    img = sup.submit("1", ["p"], [2]).result(timeout=60)
+                except ImageGenerationError:
+                    time.sleep(0.2)
+            st = sup.status()
+        finally:
+            sup.close()
+    assert img is not None and slot_of(img[0]) == 0
+    assert st["live_devices"] == ["cpu:0"] and list(st["retired"]) == ["cpu:1"], st
+    assert [p["ok"] for p in st["probes"]] == [False, True], st

@@ -81,25 +81,7 @@ def parse():
     return ap.parse_args()
 
 
-WORDS = ("lantern river tower garden mirror orchard ancient crimson hollow silent glowing ember shadow "
-         "velvet frozen radiant amber comet glacier harbor meadow falcon violin").split()
-
-
-async def player(scorer, rng, stop_at, lat, think_ms):
-    while time.perf_counter() < stop_at:
-        pairs = [(rng.choice(WORDS), rng.choice(WORDS)) for _ in range(2)]
-        t0 = time.perf_counter()
-        await scorer.score(pairs)
-        lat.append((time.perf_counter() - t0) * 1e3)
-        await asyncio.sleep(think_ms / 1e3 * rng.uniform(0.5, 1.5))
-
-
-async def run_players(scorer, n, seconds, think_ms, seed):
-    lat = []
-    stop_at = time.perf_counter() + seconds
-    rngs = [random.Random(seed * 1000 + i) for i in range(n)]
-    await asyncio.gather(*(player(scorer, r, stop_at, lat, think_ms) for r in rngs))
-    return lat
+from cassmantle_amd.runtime.live import pct, run_players  # noqa: E402  (shared with bench.py)
 
 
 def main_supervised(a) -> None:
@@ -188,8 +170,6 @@ def main_supervised(a) -> None:
     st = sup.status()
     sup.close()
 
-    def pct(x, q):
-        return float(np.percentile(np.asarray(x), q)) if x else float("nan")
     print(json.dumps({
         "metric": "live round: images/s with overlapped streaming guess scoring (BASELINE config 5)",
         "topology": "supervised", "images_per_s": round(imgs_at_stop / elapsed, 3), "n_gpus": a.gpus, "workers": n,
@@ -284,9 +264,6 @@ def main():
         sharded.close()                                # rank 0: STOP to the followers
         if follower is not None:
             follower.join(timeout=60)
-
-    def pct(x, q):
-        return float(np.percentile(np.asarray(x), q)) if x else float("nan")
 
     stats = torch.tensor([imgs_at_stop / elapsed, pct(idle, 50), pct(idle, 99), pct(load, 50), pct(load, 99),
                           float(len(load))], dtype=torch.float64, device=dev)
