@@ -509,6 +509,7 @@ def run_rank(args, wd: "Watchdog") -> int:
 
     # BASELINE configs 5 and 4 as extras of a 1-GPU record, after every headline measurement
     extras = {}
+    use_graphs, overlap = bool(sd.use_graphs), sd.decode_stream is not None
     if world == 1 and device.type == "cuda" and args.model == "sd15" and not args.baseline:
         if not args.no_live:
             extras.update(live_extra(args, sd, device, room_prompts, negative))
@@ -540,11 +541,11 @@ def run_rank(args, wd: "Watchdog") -> int:
                        "global_batch": world * args.batch, "seq_len": (spec.resolution // 8) ** 2,
                        "parallelism": f"dp{world} (rooms)"},
             "ops": ("torch-eager" if args.baseline else "hip") if device.type == "cuda" else "cpu-reference",
-            "graphs": bool(sd.use_graphs),
+            "graphs": use_graphs,
             "finite": finite,
             "s_per_image_per_gpu": round(elapsed / (args.steps * args.batch), 4),
             "batch1_s_per_image": b1,       # one room, one image, prompt -> host uint8
-            "stage_overlap": sd.decode_stream is not None,
+            "stage_overlap": overlap,
             "stage_mean_ms": stage_ms,      # device time per timed generation
             **score,
             **extras,

@@ -87,6 +87,11 @@ class GameConfig:
     # supervised groups: "async" hands each worker its rooms' next batch as soon as THAT worker
     # is idle (a slow GPU holds only its own rooms); "lockstep" runs C1/C2/C4 collective rounds
     supervisor_dispatch: str = "async"
+    # supervised async groups: how a worker's images reach the front-end.  "ipc": they stay in
+    # HBM -- the worker copies them into an outbox buffer shared once through a HIP IPC handle and
+    # the front-end lands them on ITS GPU with one device-to-device copy (xGMI between GPUs), where
+    # the blur cache reads them; "pipe": host uint8 arrays pickled through the worker's pipe
+    supervisor_transport: str = "ipc"
     # share of the rooms owned by the GPU the front-end's guess scorer also runs on (GPU 0);
     # the other GPUs have weight 1 (parallel.rooms.RoomSharding)
     frontend_device_weight: float = 0.85

@@ -23,6 +23,39 @@ class ImageGenerationError(RuntimeError):
     pass
 
 
+class DeviceImage:
+    """A generated ``uint8 [H, W, 3]`` image that stays in the front-end GPU's HBM: the supervised
+    workers' images land there over xGMI (``parallel.supervisor``, transport ``ipc``) and the blur
+    cache reads them in place.  ``np.asarray`` / :meth:`host` give the host copy (made once, for
+    the JPEG encode), so the game layer treats it like the arrays other generators return."""
+
+    __slots__ = ("tensor", "_host")
+
+    def __init__(self, tensor) -> None:
+        self.tensor = tensor
+        self._host: Optional[np.ndarray] = None
+
+    @property
+    def shape(self):
+        return tuple(self.tensor.shape)
+
+    @property
+    def dtype(self):
+        return np.dtype(np.uint8)
+
+    def host(self) -> np.ndarray:
+        if self._host is None:
+            self._host = self.tensor.cpu().numpy()
+        return self._host
+
+    def __array__(self, dtype=None, copy=None):
+        h = self.host()
+        return h if dtype is None else h.astype(dtype)
+
+    def __getitem__(self, idx):
+        return self.host()[idx]
+
+
 class ImageGenerator:
     resolution: int = 512
 

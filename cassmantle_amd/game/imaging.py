@@ -27,9 +27,10 @@ def score_to_blur(score: float, min_blur: float = 0.0, max_blur: float = 15.0) -
 
 
 def encode_jpeg(img, quality: int = 75) -> bytes:
-    """``encode_image`` parity (``src/utils.py:12-16``; PIL default quality is 75)."""
-    if isinstance(img, np.ndarray):
-        img = Image.fromarray(img)
+    """``encode_image`` parity (``src/utils.py:12-16``; PIL default quality is 75).  ``img``: a
+    PIL image, a uint8 array, or anything ``np.asarray`` turns into one (``DeviceImage``)."""
+    if not isinstance(img, Image.Image):
+        img = Image.fromarray(np.asarray(img))
     if img.mode != "RGB":
         img = img.convert("RGB")
     buf = io.BytesIO()
@@ -42,6 +43,7 @@ def decode_jpeg(data: bytes) -> np.ndarray:
 
 
 def blur_pil(img: np.ndarray, radius: float) -> np.ndarray:
+    img = np.asarray(img)
     if radius <= 0:
         return img
     return np.asarray(Image.fromarray(img).filter(ImageFilter.GaussianBlur(radius)))
@@ -67,6 +69,9 @@ class BlurCache:
         self.capacity = capacity
         self._lru: "OrderedDict[Tuple[str, float], bytes]" = OrderedDict()
         self._decoded: Tuple[Optional[str], Optional[np.ndarray]] = (None, None)
+        # version -> device-resident source image (DeviceImage) of content generated on a GPU:
+        # the blur reads it in HBM instead of decoding the JPEG (bounded: current + next content)
+        self._sources: "OrderedDict[str, object]" = OrderedDict()
         self._lock = threading.Lock()
         self.hits = 0
         self.misses = 0
@@ -74,6 +79,14 @@ class BlurCache:
     def __len__(self) -> int:
         with self._lock:
             return len(self._lru)
+
+    def set_source(self, version: str, img) -> None:
+        """Register the device-resident original of content ``version`` (see ``_sources``)."""
+        with self._lock:
+            self._sources[version] = img
+            self._sources.move_to_end(version)
+            while len(self._sources) > 4:
+                self._sources.popitem(last=False)
 
     def get(self, version: str, jpeg: bytes, radius: float) -> bytes:
         r = quantize_radius(radius, self.bucket)
@@ -84,10 +97,12 @@ class BlurCache:
                 self.hits += 1
                 return self._lru[key]
             self.misses += 1
-            ver, arr = self._decoded
-            if ver != version:
-                arr = decode_jpeg(jpeg)
-                self._decoded = (version, arr)
+            arr = self._sources.get(version)
+            if arr is None:
+                ver, arr = self._decoded
+                if ver != version:
+                    arr = decode_jpeg(jpeg)
+                    self._decoded = (version, arr)
         with TRACER.span("blur_jpeg"):
             out = encode_jpeg(self.blur_fn(arr, r), self.quality) if r > 0 else jpeg
         with self._lock:

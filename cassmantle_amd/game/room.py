@@ -151,6 +151,8 @@ class GameRoom:
             return None
         pdict = await asyncio.to_thread(self._prompt_dict, prompt)
         jpeg = await asyncio.to_thread(encode_jpeg, image, self.cfg.jpeg_quality)
+        if hasattr(image, "tensor"):           # landed in HBM (DeviceImage): blur it there
+            self.blur_cache.set_source(self._version(jpeg), image)
         return prompt, json.dumps(pdict), jpeg
 
     # ------------------------------------------------------------------ startup (backend.py:73-129)

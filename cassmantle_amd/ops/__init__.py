@@ -97,9 +97,17 @@ def record_gemms(on: bool) -> Optional[list]:
     return rec
 
 
+# diagnostic (round 6, verdict r5 item 1): CASSMANTLE_PF_SERIAL=1 reads every GEMM / conv weight
+# with ops.prefetch right before its launch, on the same stream: the in-situ GEMM times then show
+# what a MALL-warm weight is worth (the prefetch's own time is the price of doing it serially)
+_PF_SERIAL = os.environ.get("CASSMANTLE_PF_SERIAL", "0") == "1"
+
+
 def _launch(fn, *args, **kw):
     if not _tune_loaded:
         load_gemm_tuning()
+    if _PF_SERIAL:
+        prefetch(args[2] if fn is ext().gemm_cat else args[1])
     if _DIAG_TWICE:
         fn(*args, **kw)
     fn(*args, **kw)
@@ -845,6 +853,21 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
         return t.zero_()
     ext().zero_(t)
     return t
+
+
+_PREFETCH_SINK: dict = {}
+
+
+def prefetch(t: torch.Tensor, blocks: int = 64) -> None:
+    """Read ``t`` once (one dword per 64-B segment) on the current stream so its lines sit in the
+    memory-side cache / L2 when a later kernel reads them: the next layer's weights, warmed on a
+    side stream while the current layer runs (a no-op off the HIP path)."""
+    if not _use_hip(t):
+        return
+    sink = _PREFETCH_SINK.get(t.device)
+    if sink is None:
+        sink = _PREFETCH_SINK[t.device] = torch.zeros(4, device=t.device, dtype=torch.int32)
+    ext().prefetch(t, sink, int(blocks))
 
 
 def advance_step(step: torch.Tensor) -> None:

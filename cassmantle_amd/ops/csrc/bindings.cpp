@@ -755,6 +755,15 @@ void zero_(at::Tensor& t) {
   launch_zero(t.data_ptr(), (long long)t.numel() * (long long)t.element_size(), cur_stream());
 }
 
+void prefetch(const at::Tensor& t, at::Tensor& sink, int64_t blocks) {
+  CHECK_DEV(t);
+  CHECK_CONTIG(t);
+  CHECK_DEV(sink);
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 3) == 0 && sink.numel() * sink.element_size() >= 4, "prefetch: aligned tensor, 4-B sink");
+  launch_prefetch(t.data_ptr(), (long long)t.numel() * (long long)t.element_size(), (int)blocks, sink.data_ptr(),
+                  cur_stream());
+}
+
 void softmax_rows(const at::Tensor& S, at::Tensor& P, int64_t causal, const c10::optional<at::Tensor>& kv_lens) {
   CHECK_DEV(S); CHECK_CONTIG(S); CHECK_CONTIG(P);
   TORCH_CHECK(S.scalar_type() == at::kFloat, "softmax_rows: f32 scores");
@@ -885,6 +894,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("latent_step", &latent_step, nogil());
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());
+  m.def("prefetch", &prefetch, nogil());
   m.def("cu_mask_stream", &cu_mask_stream);
   m.def("cu_count", &cu_count);
   m.def("softmax_rows", &softmax_rows, nogil());

@@ -56,6 +56,15 @@ CM_DEVICE int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 // 32/G N-panels instead of 2 x 16 (less A+W per XCD L2 on small grids).  G = p.raster, or
 // GEMM_RASTER_G when 0.  G = 4 measured 524.9 -> 521.6 ms/step on the bench, same box x2
 // (profiles/r5_raster_ab.txt)
+// Warp-specialised tiles (NP > 0): the MFMA waves issue no global loads in the mainloop, so at the
+// kernel start they read their block's W panel once (one dword per 64-B line, the block's k
+// range; GEMM_PF_SELF 2: only the quarter selected by tm & 3, the M tiles of one XCD's raster
+// group sharing the panel) to bring the weights to L2 / MALL while the DMA ring starts.  The
+// loads are waited for only at the end (their XOR feeds an empty asm): a cold weight's HBM
+// latency then overlaps the ring instead of stalling k-tiles.
+#ifndef GEMM_PF_SELF
+#define GEMM_PF_SELF 0
+#endif
 #ifndef GEMM_RASTER_G
 #define GEMM_RASTER_G 4
 #endif
@@ -824,6 +833,28 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
   if constexpr (CONV >= 2) tap_init(kt0);
 
+#if GEMM_PF_SELF
+  uint32_t pf_acc = 0;
+  if constexpr (NP > 0 && !GEGLU) {
+    if (mma_wave && nk > 0) {
+      const int kb = kt0 * BK, ke = min(p.K, (kt0 + nk) * BK);
+      const int lpr = ((ke - kb) * 2 + 63) / 64;          // 64-B lines per W row in this k range
+      const int rows = min(BN, p.Nw - n0);
+      int l0 = 0, l1 = rows * lpr;
+      if (GEMM_PF_SELF == 2) {
+        const int part = (l1 + 3) / 4;
+        l0 = (tm & 3) * part;
+        l1 = min(l1, l0 + part);
+      }
+      const uint32_t* Wp = reinterpret_cast<const uint32_t*>(W);
+      for (int l = l0 + tid; l < l1; l += 64 * NW) {
+        const int r = l / lpr, c = l - r * lpr;
+        pf_acc ^= Wp[((long long)(n0 + r) * ldw + kb) / 2 + c * 16];
+      }
+    }
+  }
+#endif
+
   if constexpr (STAGES == 2) {
     if (nk > 0) stage(kt0, 0);
     __syncthreads();                       // drains the DMA (vmcnt(0)) and publishes the tile
@@ -870,6 +901,9 @@ gemm_kernel(GemmArgs p, float* __restrict__ partial) {
 
   tile_epilogue<BM, BN, WM, WN, GEGLU, OUTF32, TI, TJ, THREADS>(p, acc, smem, partial, m0, n0, batch, wm, wn, tid,
                                                                gridDim.y, blockIdx.y, mma_wave);
+#if GEMM_PF_SELF
+  asm volatile("" ::"v"(pf_acc));         // keeps the warm-up loads; their wait lands here
+#endif
 }
 
 // split-K: a second, fully parallel pass sums the slices' fp32 slabs and applies the epilogue

@@ -202,5 +202,6 @@ void launch_latent_step(const uint16_t* eps, float* x, float* hist, float* xs, c
                         hipStream_t s);
 void launch_advance_step(int* step, hipStream_t s);
 void launch_zero(void* p, long long bytes, hipStream_t s);
+void launch_prefetch(const void* p, long long bytes, int blocks, void* sink, hipStream_t s);
 void launch_softmax_rows(const float* S, uint16_t* P, int rows, int cols, int Nq, int causal,
                          const int* kv_lens, hipStream_t s);

@@ -132,6 +132,23 @@ def generate_local(gen: ImageGenerator, jobs: Sequence["GenJob"], negative: str)
         return [None] * len(jobs)
 
 
+def generate_local_device(gen: ImageGenerator, jobs: Sequence["GenJob"], negative: str):
+    """``generate_local`` for a device-resident generator without the host copy: the uint8
+    [n, H, W, 3] images in this worker's HBM once their completion event fired, or ``None`` when
+    the generation raised or its latents are not finite (the rooms repeat their content)."""
+    if not jobs:
+        return None
+    try:
+        out = gen.generate_device([j.prompt for j in jobs], negative, [j.seed for j in jobs])
+        wait_event(out.event)
+        if out.finite is not None and not bool(out.finite.reshape(-1)[0]):
+            raise ImageGenerationError("non-finite latents")
+        return out.images
+    except Exception as e:  # noqa: BLE001 - reported as failed jobs, the worker stays up
+        log.error("[ERROR] local generation failed: %s", e)
+        return None
+
+
 class RankWorker:
     """Executes generation rounds; identical code on every rank.
 

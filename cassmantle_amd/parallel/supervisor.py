@@ -41,6 +41,17 @@ Two dispatch modes:
   job list from the leader, local generation, C2 device-resident RCCL gather to the leader, C4
   barrier (the headline ``bench.py`` runs the same collectives).
 
+Data plane of the async mode (``transport``): ``ipc`` keeps a worker's images in HBM end to end.
+The worker copies each round's uint8 images into an outbox buffer in its own HBM, shared with
+the front-end ONCE (a HIP IPC handle, torch's CUDA-tensor reduction over the pipe; re-shared only
+when it grows), and the pipe carries just the round id and shape.  The front-end lands the images
+on its own GPU with one device-to-device copy -- over xGMI when the worker sits on another GPU --
+and hands ``DeviceImage`` handles to the game layer, whose blur cache reads them in place (the
+JPEG of the content needs one host copy).  The worker reuses its outbox only for its next round,
+which is dispatched after the front-end's copy completed.  ``pipe`` sends host arrays instead
+(a CPU front-end, or ``GameConfig.supervisor_transport = "pipe"``).  On the CPU (tests) the
+outbox is a shared-memory tensor: the same protocol.
+
 The legacy ``torchrun`` layout (front-end inside rank 0, ``serve.py`` under torchrun) is still
 supported; there a dead rank can only degrade the node to rank 0's GPU.
 """
@@ -92,6 +103,39 @@ class WorkerSpec:
     env: Dict[str, str] = field(default_factory=dict)
     dispatch: str = "async"         # async | lockstep (module docstring)
     weights: Optional[List[float]] = None
+    transport: str = "pipe"         # async data plane: ipc | pipe (module docstring)
+
+
+class DeviceOutbox:
+    """Worker end of the ``ipc`` data plane: one uint8 buffer in this worker's memory (HBM, or
+    shared memory on the CPU) that every round's images are copied into.  ``put`` returns the
+    buffer when it was (re)allocated -- the front-end must be sent the new mapping -- else None."""
+
+    def __init__(self, device) -> None:
+        import torch
+        self.device = torch.device(device)
+        self.buf = None
+        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+
+    def put(self, images):
+        import torch
+        n = images.numel()
+        fresh = None
+        if self.buf is None or self.buf.numel() < n:
+            cap = max(n, 2 * self.buf.numel()) if self.buf is not None else n
+            self.buf = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            if self.device.type == "cpu":
+                self.buf.share_memory_()
+            fresh = self.buf
+        if self.stream is not None:
+            # the images are complete (their event was waited on); the copy is ordered on this
+            # stream and finished before the front-end is told about it
+            with torch.cuda.stream(self.stream):
+                self.buf[:n].copy_(images.reshape(-1), non_blocking=True)
+            self.stream.synchronize()
+        else:
+            self.buf[:n].copy_(images.reshape(-1))
+        return fresh
 
 
 def default_generator(cfg, device: str, spec: WorkerSpec) -> ImageGenerator:
@@ -114,7 +158,7 @@ def worker_main(spec: WorkerSpec, conn, hb, progress) -> None:
     import torch.distributed as dist
 
     from .dist import DistContext
-    from .rooms import STOP, RankWorker, RoomSharding, generate_local
+    from .rooms import STOP, RankWorker, RoomSharding, generate_local, generate_local_device
 
     stop_hb = threading.Event()
 
@@ -140,15 +184,29 @@ def worker_main(spec: WorkerSpec, conn, hb, progress) -> None:
         dist.barrier()                                   # every member is up
         if spec.dispatch == "async":
             # the front-end drives this worker alone: no collective after the handshake
+            outbox = None
+            if spec.transport == "ipc" and hasattr(gen, "generate_device"):
+                import torch.multiprocessing  # noqa: F401 - tensor reductions (IPC / shm) for the pipe
+                outbox = DeviceOutbox(dev)
             conn.send(("ready", os.getpid()))
             while True:
                 msg = conn.recv()
                 if msg[0] == "stop":
                     break
                 _, rid, jobs = msg
-                imgs = generate_local(gen, jobs, spec.negative)
-                done(rid)                                # device work finished (or failed)
-                conn.send(("result", rid, imgs, None))
+                if outbox is None:
+                    imgs = generate_local(gen, jobs, spec.negative)
+                    done(rid)                            # device work finished (or failed)
+                    conn.send(("result", rid, imgs, None))
+                    continue
+                dimg = generate_local_device(gen, jobs, spec.negative)
+                if dimg is None:
+                    done(rid)
+                    conn.send(("result", rid, [None] * len(jobs), None))
+                    continue
+                fresh = outbox.put(dimg)
+                done(rid)
+                conn.send(("result_dev", rid, {"shape": tuple(dimg.shape), "buf": fresh}, None))
             dist.destroy_process_group()
             stop_hb.set()
             os._exit(0)
@@ -208,7 +266,7 @@ class _Group:
         for r, d in enumerate(devices):
             spec = WorkerSpec(r, W, port, sup.device_name(d), sup.backend, sup.room_ids, sup.negative,
                               sup.gen_factory, sup.cfg, epoch, d, sup.heartbeat_s, dict(sup.worker_env),
-                              sup.dispatch, weights)
+                              sup.dispatch, weights, sup.transport if per_worker else "pipe")
             child = children[r] if per_worker else (children[0] if r == 0 else None)
             p = ctx.Process(target=worker_main, args=(spec, child, self.hb, self.progress),
                             name=f"cassmantle-w{r}e{epoch}", daemon=True)
@@ -282,9 +340,18 @@ class GroupSupervisor:
                  max_restarts_without_culprit: int = 2, local: Optional[ImageGenerator] = None,
                  worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None,
                  reprobe_s: float = 120.0, dispatch: str = "async",
-                 weights: Optional[Dict[str, float]] = None) -> None:
+                 weights: Optional[Dict[str, float]] = None, transport: str = "pipe",
+                 frontend_device: Optional[str] = None) -> None:
         if dispatch not in ("async", "lockstep"):
             raise ValueError(f"dispatch must be async or lockstep, not {dispatch!r}")
+        if transport not in ("ipc", "pipe"):
+            raise ValueError(f"transport must be ipc or pipe, not {transport!r}")
+        # ``ipc``: images land on ``frontend_device`` (the front-end's GPU; None / cpu: host arrays)
+        self.transport = transport
+        self.frontend_device = frontend_device
+        self._inbox: Dict[Tuple[int, int], Any] = {}   # (epoch, worker) -> its outbox, mapped here
+        self._land_stream = None
+        self.land_us: List[float] = []
         self.cfg = cfg
         self.all_devices = list(devices)
         if len(set(self.all_devices)) != len(self.all_devices):
@@ -785,9 +852,22 @@ class GroupSupervisor:
                     except (EOFError, OSError) as e:
                         failure = self._diagnose(g, rid, f"worker {w} pipe: {type(e).__name__}", suspects=[w])
                         break
-                    if msg[0] == "result" and msg[1] == rid:
+                    if msg[0] in ("result", "result_dev") and msg[1] == rid:
                         del busy[w]
-                        imgs = msg[2]
+                        if msg[0] == "result":
+                            imgs = msg[2]
+                        else:
+                            try:
+                                imgs = self._land(g, w, msg[2])
+                            except Exception as e:  # noqa: BLE001 - IPC mapping / copy failed
+                                log.exception("[ERROR] landing worker %d's images failed; falling back to "
+                                              "the pipe transport", w)
+                                self.transport = "pipe"   # the restarted group sends host arrays
+                                for s0, e0, room, fut in spans:
+                                    if not fut.done():
+                                        fut.set_exception(ImageGenerationError(f"image transport failed: {e}"))
+                                failure = GroupFailure(f"ipc transport: {type(e).__name__}: {e}", [])
+                                break
                         self._round_ok()
                         dev = g.devices[w]
                         self.worker_rounds[dev] = self.worker_rounds.get(dev, 0) + 1
@@ -828,6 +908,34 @@ class GroupSupervisor:
             for *_, fut in spans:
                 if not fut.done():
                     fut.set_exception(ImageGenerationError("supervisor closed"))
+
+    def _land(self, g: "_Group", w: int, payload: Dict[str, Any]) -> List[Any]:
+        """``ipc`` transport, front-end side: the worker's round is in its outbox (mapped here
+        once per outbox allocation); one device-to-device copy lands it on ``frontend_device``
+        (xGMI when the worker's GPU differs) -> ``DeviceImage`` per image; host arrays without a
+        front-end GPU."""
+        import torch
+        from ..game.content import DeviceImage
+        key = (g.epoch, w)
+        if payload["buf"] is not None:
+            self._inbox = {k: v for k, v in self._inbox.items() if k[0] == g.epoch and k != key}
+            self._inbox[key] = payload["buf"]
+        shape = tuple(payload["shape"])
+        n = int(np.prod(shape))
+        src = self._inbox[key][:n].view(shape)
+        dev = torch.device(self.frontend_device) if self.frontend_device else None
+        if dev is None or dev.type != "cuda":
+            host = src.cpu().numpy()
+            return [host[i].copy() for i in range(shape[0])]
+        if self._land_stream is None:
+            self._land_stream = torch.cuda.Stream(device=dev)
+        t0 = time.perf_counter()
+        dst = torch.empty(shape, dtype=torch.uint8, device=dev)
+        with torch.cuda.stream(self._land_stream):
+            dst.copy_(src, non_blocking=True)
+        self._land_stream.synchronize()      # the worker may overwrite its outbox from its next round
+        self.land_us.append((time.perf_counter() - t0) * 1e6)
+        return [DeviceImage(dst[i]) for i in range(shape[0])]
 
     def _loop(self) -> None:
         try:
@@ -886,7 +994,9 @@ class GroupSupervisor:
                 "dispatch": self.dispatch, "worker_rounds": dict(self.worker_rounds),
                 "owners": ({r: self.group.devices[self.sharding.owner(r)] for r in self.room_ids}
                            if self.group is not None else {}),
-                "gather_us_p50": float(np.median(self.gather_us)) if self.gather_us else None}
+                "gather_us_p50": float(np.median(self.gather_us)) if self.gather_us else None,
+                "transport": self.transport if self.dispatch == "async" else "rccl-gather",
+                "land_us_p50": float(np.median(self.land_us)) if self.land_us else None}
 
 
 class SupervisedImageGenerator(ImageGenerator):

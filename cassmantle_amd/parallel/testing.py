@@ -103,7 +103,10 @@ def stamped_generator(cfg, device: str, spec) -> StampedGenerator:
     time.sleep(float(os.environ.get("CASSMANTLE_FAULT_START_DELAY", "0")))
     if os.environ.get("CASSMANTLE_FAULT") == "start_kill" and _faulty(slot) and trig and os.path.exists(trig):
         os._exit(17)                     # dies without reporting, before the "ready" message
-    cls = AsyncStampedGenerator if os.environ.get("CASSMANTLE_FAULT") == "async_hang" else StampedGenerator
+    # CASSMANTLE_DEVICE_GEN=1: the device-resident interface without a fault (the ``ipc`` data
+    # plane of the supervisor, host tensors standing in for HBM)
+    dev_gen = os.environ.get("CASSMANTLE_FAULT") == "async_hang" or os.environ.get("CASSMANTLE_DEVICE_GEN") == "1"
+    cls = AsyncStampedGenerator if dev_gen else StampedGenerator
     return cls(spec.slot or device, res=cfg.model.resolution)
 
 

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from typing import Callable, Optional
 
+import numpy as np
 import torch
 
 from ..config import Config
@@ -84,7 +85,11 @@ def build_blur_fn(cfg: Config, device: Optional[str] = None):
 
     def blur(img, radius: float):
         with torch.cuda.stream(stream):
-            x = torch.from_numpy(img).to(dev, non_blocking=False)
+            t = getattr(img, "tensor", None)        # DeviceImage: already in this GPU's HBM
+            if t is not None and t.device.type == "cuda":
+                x = t.to(dev, non_blocking=False)
+            else:
+                x = torch.from_numpy(np.ascontiguousarray(np.asarray(img))).to(dev, non_blocking=False)
             y = ops.gaussian_blur(x, radius)
             return y.cpu().numpy()
     return blur

@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--shard-min", type=int, default=256)
     ap.add_argument("--dispatch", choices=("async", "lockstep"), default="async",
                     help="supervised topology: per-worker (async) or collective (lockstep) rounds")
+    ap.add_argument("--transport", choices=("ipc", "pipe"), default="ipc",
+                    help="supervised async data plane: images land on GPU 0 from the workers' HBM "
+                         "outboxes (ipc) or travel as host arrays through the pipes (pipe)")
     ap.add_argument("--weight0", type=float, default=None,
                     help="room share of GPU 0 (the scorer's device); default config.frontend_device_weight")
     ap.add_argument("--slots-per-gpu", type=int, default=1,
@@ -111,7 +114,8 @@ def main_supervised(a) -> None:
     t_start = time.perf_counter()
     w0 = cfg.game.frontend_device_weight if a.weight0 is None else a.weight0
     sup = GroupSupervisor(cfg, devices, rooms, window_s=0.05, start_timeout_s=1200, dispatch=a.dispatch,
-                          weights={devices[0]: w0})
+                          weights={devices[0]: w0}, transport=a.transport,
+                          frontend_device="cuda:0" if gpu else None)
     if not sup.wait_ready(1500) or not sup.live_devices():
         raise SystemExit(f"worker group did not start: {sup.status()}")
     print(f"[live] worker group up on {sup.live_devices()} in {time.perf_counter() - t_start:.1f} s",
@@ -178,7 +182,8 @@ def main_supervised(a) -> None:
         "load_p50_ms": round(pct(load, 50), 3), "load_p99_ms": round(pct(load, 99), 3), "requests": len(load),
         "rounds": done["rounds"], "gather_us_p50": st["gather_us_p50"], "retired": st["retired"],
         "scorer_stream_priority": prio, "seconds": a.seconds, "dispatch": a.dispatch,
-        "worker_rounds": st.get("worker_rounds"),
+        "worker_rounds": st.get("worker_rounds"), "transport": st.get("transport"),
+        "land_us_p50": st.get("land_us_p50"),
         "config": {"model": a.model, "batch_per_room": a.batch, "rooms": len(rooms)}}), flush=True)
 
 

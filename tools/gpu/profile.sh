@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o run --output-format csv -- \
-  python bench.py --model $model --steps 1 --warmup 1 --denoise-steps $steps --no-score --no-batch1 "$@" \
+  python bench.py --model $model --steps 1 --warmup 1 --denoise-steps $steps --no-score --no-batch1 --no-live --no-sdxl "$@" \
   > gpurun_out/prof_$name.log 2>&1 || { tail -20 gpurun_out/prof_$name.log; exit 1; }
 grep '^{' gpurun_out/prof_$name.log | head -c 400; echo
 f=$(find gpurun_out/prof_$name -name '*kernel_trace.csv' | head -1)
