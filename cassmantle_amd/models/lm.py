@@ -205,19 +205,10 @@ class LMTextGenerator:
     # one decode step entirely on device buffers (captured as a graph on GPU)
     def _step(self) -> None:
         logits = self.model(self.tok_buf.view(1, 1), self.kc, self.vc, self.pos, self.lens, decode=True)
-        lg = logits.float() / self.temperature
-        eos = self.tok.eos
-        if 0 <= eos < lg.shape[-1]:
-            lg[:, eos] += self.eos_bias.index_select(0, self.idx)
-        vals, ids = lg.topk(self.top_k, dim=-1)
-        g = self.noise.index_select(0, self.idx)[0].gather(1, ids)     # Gumbel noise of this step
-        choice = (vals + g).argmax(dim=-1, keepdim=True)
-        nxt = ids.gather(1, choice)[:, 0]
-        self.out.index_copy_(0, self.idx, nxt[None])
-        self.tok_buf.copy_(nxt)
-        self.pos.add_(1)
-        self.lens.add_(1)
-        self.idx.add_(1)
+        # top-k + Gumbel-max with this step's noise row, and the token / position / length / step
+        # update: one in-tree kernel on the GPU (lm.hip lm_sample_kernel), no ATen sampling ops
+        ops.lm_sample(logits, self.noise, self.eos_bias, self.tok.eos, self.temperature, self.top_k, self.idx,
+                      self.out, self.tok_buf, self.pos, self.lens)
 
     def _capture(self) -> None:
         s = torch.cuda.Stream()

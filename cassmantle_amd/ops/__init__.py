@@ -580,6 +580,17 @@ def rope_kv(qkv: torch.Tensor, pos0: torch.Tensor, q_out: torch.Tensor, k_cache:
     ext().rope_kv(qkv, pos0, q_out, k_cache, v_cache, int(heads), int(kv_heads), float(theta))
 
 
+def lm_sample(logits: torch.Tensor, noise: torch.Tensor, eos_bias: torch.Tensor, eos: int, temperature: float,
+              k: int, step: torch.Tensor, out: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor,
+              lens: torch.Tensor) -> None:
+    """One decode step's sampling (top-k + Gumbel-max) and device-state update, batch 1:
+    ``ops.reference.lm_sample`` is the contract; on the GPU one in-tree kernel (lm.hip)."""
+    if not _use_hip(logits):
+        return ref.lm_sample(logits, noise, eos_bias, eos, temperature, k, step, out, tok, pos, lens)
+    ext().lm_sample(logits.contiguous(), noise, eos_bias, int(eos), float(temperature), int(k), step, out, tok, pos,
+                    lens)
+
+
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
                      scale: Optional[float] = None) -> torch.Tensor:
     """One query token per sequence.  q [B, H, d]; caches [B, L, Hk, d]; lens [B] int32 (device)
@@ -609,11 +620,12 @@ FP8_ATTN_VARIANTS = ("8x1", "4x1", "4x2", "2x2", "2x4", "1x4")
 
 
 def set_attention_d40_variant(variant: Optional[str]) -> None:
-    """Head dim 40 (SD-1.5 level 1): ``"16x16"`` (default), ``"32x32"`` or ``"mixed"`` (32x32x16
-    QK^T, 16x16x32 P.V) kernel; None restores the default (``CASSMANTLE_ATTN16`` = 1 / 0 / 2).
-    A/B knob for tests and tools/bench_attn.py."""
+    """Head dim 40 (SD-1.5 level 1): ``"16x16"`` (default) or ``"32x32"`` (the generic kernel at
+    d = 40, which also serves causal masks); None restores the default (``CASSMANTLE_ATTN16`` =
+    1 / 0).  A/B knob for tests and tools/bench_attn.py.  (The round-5 ``"mixed"`` kernel is
+    archived unbuilt: tools/archive/attn_mx_d40.hip.txt.)"""
     if ext_available():
-        ext().set_attn_d40_variant({None: -1, "16x16": 1, "32x32": 0, "mixed": 2}[variant])
+        ext().set_attn_d40_variant({None: -1, "16x16": 1, "32x32": 0}[variant])
 
 
 def set_fp8_attention_variant(variant: Optional[str]) -> None:

@@ -598,7 +598,10 @@ __global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
       }
     }
     const int kbase = t * KT;
-    if (kbase + KT > nk) {
+    if (__builtin_expect(kbase + KT > nk, 0)) {
+      // a real branch: without the volatile asm hipcc if-converts this block and pays its 16
+      // compares + 32 v_cndmask on EVERY tile (round 6, ISA of attn16_d40_kernel<8>)
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -706,272 +709,6 @@ template <int NW>
 void launch_a16(const AttnArgs& a, hipStream_t s) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   hipLaunchKernelGGL((attn16_d40_kernel<NW>), dim3(nqb * a.H * a.B), dim3(64 * NW), 0, s, a);
-}
-
-// ======================================================================= head dim 40, mixed shapes
-// The layout the round-4 review asked to be built and measured: QK^T on 32x32x16 MFMAs (the
-// 32x32 kernel's, 6 per 64-key tile: 192 pipe / 48 issue cycles), P.V on 16x16x32 MFMAs over 48
-// O^T rows (the 16x16 kernel's, 12 per tile: 192 / 96), so neither the 32x32 kernel's 16 padded
-// O^T rows nor the 16x16 kernel's 32-deep d = 40 tail step is paid (448 pipe cycles per tile in
-// both).  The price is relaying P^T between the two accumulator layouts:
-//   S^T (32x32): lane l holds query l & 31, keys 8i + 4h + r of each 32-key block (h = l >> 5)
-//   packed bf16 X = keys of i = 0, 1 and Y = keys of i = 2, 3; one v_permlane16_swap per register
-//   pair exchanges X's odd 16-lane rows with Y's even rows, after which X is the 16x16x32 B
-//   operand of queries 0-15 and Y that of queries 16-31: row g holds keys base_g + {0..3, 8..11},
-//   base = 0, 16, 4, 20 -- and V^T is read in that key order (two tr reads, rows base_g + (li>>2)
-//   and 8 further).  Per tile 8 swaps; the rare rescale path moves alpha to the O layout (query
-//   16 qb + li) with two lane shuffles.
-// Measured (same box, x4 interleaved, profiles/r5_attn_d40_mixed_ab.jsonl): 1.2-3.5 % SLOWER than
-// the 16x16 kernel on the level-1 self-attention (MFMA busy 40.7 vs 46.3 %, VALU per MFMA 6.6 vs
-// 4.5: the relay and the 32x32 accumulators' extra moves outweigh 80 fewer MFMA issue cycles),
-// 2-3 % faster on the 77-key cross-attention.  Kept selectable ("mixed"), not the default.
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 2) attn_mx_d40_kernel(AttnArgs a) {
-  constexpr int THREADS = 64 * NW;
-  constexpr int QB = 32 * NW;
-  // LDS: K rows of 56 elements; V row r at 48 r + 32 (r >> 3) (the relaid key order puts rows r
-  // and r + 8 / r + 16 in one tr-read pass; the 64-B step per 8 rows cut this kernel's LDS bank
-  // conflicts from 49.8 % to 14.7 % of LDS cycles, profiles/r5_attn_d40_mixed_ab.jsonl)
-  constexpr int KSTR = 56;
-  constexpr int KTILE = KT * KSTR;
-  constexpr int VTILE = KT * A16_STR + 32 * (KT / 8);
-  constexpr int BUF = KTILE + VTILE;
-  constexpr int CH = KT * A16_NCH;
-  constexpr int LD = (CH + THREADS - 1) / THREADS;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int hlf = lane >> 5, ql = lane & 31;      // S (32x32) layout
-  const int g = lane >> 4, li = lane & 15;        // O (16x16) layout
-
-  const int nqb = (a.Nq + QB - 1) / QB;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qblk = bid % nqb;
-  const int bh = bid / nqb;
-  const int h = bh % a.H;
-  const int b = bh / a.H;
-  const int q0 = qblk * QB + wave * 32;
-
-  int nk = a.Nk;
-  if (a.kv_lens) nk = min(nk, a.kv_lens[b]);
-  const int ntiles = (nk + KT - 1) / KT;
-
-  const uint16_t* Qp = a.q + (long long)b * a.q_sb + (long long)h * a.q_sh;
-  const int hk = a.group > 1 ? h / a.group : h;
-  const uint16_t* Kp = a.k + (long long)b * a.k_sb + (long long)hk * a.k_sh;
-  const uint16_t* Vp = a.v + (long long)b * a.v_sb + (long long)hk * a.v_sh;
-
-  // Q^T fragments (B operand of the 32x32x16 QK^T): query q0 + ql, d 16 ks + 8 hlf .. +7,
-  // pre-scaled by scale*log2(e); d 40 (k-step 2, upper half, element 0) carries -m
-  const float qs = a.scale * 1.4426950408889634f;
-  bf16x8_t qf[3];
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    const int q = q0 + ql;
-    const int d0 = 16 * ks + 8 * hlf;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (q < a.Nq && d0 < 40) v = *reinterpret_cast<const uint4*>(Qp + (long long)q * a.q_sn + d0);
-    float f[8];
-    unpack8(v, f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] *= qs;
-    qf[ks] = as_bf16x8(pack8(f));
-  }
-
-  // the constant column chunk (d 40 = 1.0, 41..47 = 0) of every row of both buffers' K and V
-  auto vrow = [](int key) { return key * A16_STR + 32 * (key >> 3); };
-  for (int r = tid; r < 2 * 2 * KT; r += THREADS) {
-    const int buf = r / (2 * KT), rr = r % (2 * KT);
-    const int off = buf * BUF + (rr < KT ? rr * KSTR : KTILE + vrow(rr - KT));
-    *reinterpret_cast<uint4*>(lds + off + 40) = make_uint4(0x3F80u, 0, 0, 0);
-  }
-
-  uint4 kr[LD], vr[LD];
-  int c_key[LD], c_lds[LD], c_vlds[LD];
-  long long c_ks[LD], c_vs[LD];
-#pragma unroll
-  for (int i = 0; i < LD; ++i) {
-    const int c = tid + i * THREADS;
-    const int key = c / A16_NCH, ch = c - key * A16_NCH;
-    c_key[i] = c < CH ? key : (1 << 30);
-    c_lds[i] = c < CH ? key * KSTR + ch * 8 : -1;
-    c_vlds[i] = c < CH ? KTILE + vrow(key) + ch * 8 : -1;
-    c_ks[i] = (long long)key * a.k_sn + ch * 8;
-    c_vs[i] = (long long)key * a.v_sn + ch * 8;
-  }
-  auto gload = [&](int t) {
-    const int kbase = t * KT;
-    const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
-#pragma unroll
-    for (int i = 0; i < LD; ++i) {
-      uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
-      if (kbase + c_key[i] < nk) {
-        x = *reinterpret_cast<const uint4*>(Kp + ko + c_ks[i]);
-        y = *reinterpret_cast<const uint4*>(Vp + vo + c_vs[i]);
-      }
-      kr[i] = x;
-      vr[i] = y;
-    }
-  };
-  auto lstore = [&](int bo) {
-#pragma unroll
-    for (int i = 0; i < LD; ++i)
-      if (c_lds[i] >= 0) {
-        *reinterpret_cast<uint4*>(lds + bo + c_lds[i]) = kr[i];
-        *reinterpret_cast<uint4*>(lds + bo + c_vlds[i]) = vr[i];
-      }
-  };
-
-  if (ntiles > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  if constexpr (NW == 8 && ATTN_PRIO) {
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
-
-  f32x4_t oacc[3][2];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) oacc[i][qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = 0.f;
-  constexpr float RESCALE_THR = 8.f;
-  // V^T tr reads in the relaid key order: group g reads key rows base_g + (li >> 2) (+ 8)
-  const int base_g = 16 * (g & 1) + 4 * (g >> 1);
-  const int tr_off = vrow(base_g + (li >> 2)) + 4 * (li & 3);
-  constexpr int V_HI = 8 * A16_STR + 32;             // row + 8
-  constexpr int V_KB = 32 * A16_STR + 32 * 4;        // row + 32
-
-  for (int t = 0; t < ntiles; ++t) {
-    const bool more = t + 1 < ntiles;
-    if (more) gload(t + 1);
-    const int bo = (t & 1) * BUF;
-    const uint16_t* Ks = lds + bo;
-    const uint16_t* Vs = lds + bo + KTILE;
-
-    // ---- S^T - m for 2 x 32 keys x 32 queries
-    f32x16_t sacc[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
-      const uint16_t* krow = Ks + (32 * kb + ql) * KSTR + 8 * hlf;
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        const bf16x8_t kf = as_bf16x8(*reinterpret_cast<const uint4*>(krow + 16 * ks));
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sacc[kb], 0, 0, 0);
-      }
-    }
-    const int kbase = t * KT;
-    if (kbase + KT > nk) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + 32 * kb + 8 * (r >> 2) + 4 * hlf + (r & 3) >= nk) sacc[kb][r] = -INFINITY;
-    }
-
-    // ---- deferred-max online softmax (lane-local test; the query's other 32 keys in lane ^ 32)
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
-    if (__builtin_expect(t == 0 || !__all(mx <= RESCALE_THR), 0)) {
-      asm volatile("" ::: "memory");
-      const float2 hm = both_halves(mx);
-      const float m = fmaxf(hm.x, hm.y);
-      float delta = (t == 0) ? m : fmaxf(m, 0.f);
-      if (!(delta > -1e30f)) delta = 0.f;            // fully masked tile for this query
-      const float mn = (float)(__bf16)(m_run + delta);   // an MFMA operand: keep it bf16-exact
-      delta = mn - m_run;
-      m_run = mn;
-      if (hlf) qf[2][0] = (__bf16)(-mn);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      // O rows are queries 16 qb + li: fetch their alphas from the S layout (query = lane & 31)
-      const float a0 = __shfl(alpha, li, 64), a1 = __shfl(alpha, 16 + li, 64);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          oacc[i][0][r] *= a0;
-          oacc[i][1][r] *= a1;
-        }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[kb][r] -= delta;
-    }
-
-    // ---- P^T: exp2, pack, relay to the 16x16x32 B layout (X -> queries 0-15, Y -> 16-31)
-    bf16x8_t pb[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      unsigned xw[4], yw[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        xw[v] = pack2(__builtin_amdgcn_exp2f(sacc[kb][2 * v]), __builtin_amdgcn_exp2f(sacc[kb][2 * v + 1]));
-        yw[v] = pack2(__builtin_amdgcn_exp2f(sacc[kb][8 + 2 * v]), __builtin_amdgcn_exp2f(sacc[kb][8 + 2 * v + 1]));
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const auto r = __builtin_amdgcn_permlane16_swap(xw[v], yw[v], false, false);
-        xw[v] = r[0];
-        yw[v] = r[1];
-      }
-      pb[kb][0] = as_bf16x8(make_uint4(xw[0], xw[1], xw[2], xw[3]));
-      pb[kb][1] = as_bf16x8(make_uint4(yw[0], yw[1], yw[2], yw[3]));
-    }
-
-    // ---- O^T += V^T P^T over 48 d rows, one 32-deep k-step per 32-key block
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int db = 0; db < 3; ++db) {
-        const uint16_t* base = Vs + kb * V_KB + 16 * db + tr_off;
-        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(base));
-        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(base + V_HI));
-        typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-        s16x8_t vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          oacc[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[kb][qb], oacc[db][qb], 0, 0, 0);
-      }
-    if (more) lstore(BUF - bo);
-    __syncthreads();
-  }
-
-  // ---- epilogue: O[q][d] = O^T[d][q] / l, l = O^T row 40 (lanes 32..47, register 0 of block 2)
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const float ls = __shfl(oacc[2][qb][0], 32 + li, 64);
-    const int q = q0 + 16 * qb + li;
-    if (q >= a.Nq) continue;
-    const float inv = ls > 0.f ? 1.f / ls : 0.f;
-    uint16_t* Op = a.o + (long long)b * a.o_sb + (long long)q * a.o_sn + (long long)h * a.o_sh;
-#pragma unroll
-    for (int db = 0; db < 3; ++db) {
-      const int dd = 16 * db + 4 * g;
-      if (dd < 40) {
-        uint2 w;
-        w.x = pack2(oacc[db][qb][0] * inv, oacc[db][qb][1] * inv);
-        w.y = pack2(oacc[db][qb][2] * inv, oacc[db][qb][3] * inv);
-        *reinterpret_cast<uint2*>(Op + dd) = w;
-      }
-    }
-  }
-}
-
-template <int NW>
-void launch_mx(const AttnArgs& a, hipStream_t s) {
-  const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
-  hipLaunchKernelGGL((attn_mx_d40_kernel<NW>), dim3(nqb * a.H * a.B), dim3(64 * NW), 0, s, a);
 }
 
 template <int DQK, int DO, int NW>
@@ -1223,7 +960,10 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
       }
       const int kbase = t * KT;
       const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
-      if (need_mask) {
+      if (__builtin_expect(need_mask, 0)) {
+        // a real branch (see attn16_d40_kernel): if-converted, this mask cost ~130 VALU + 66 SALU
+        // per 64-key tile on unmasked tiles, more than the softmax itself (round 6 ISA count)
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
@@ -1463,10 +1203,8 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
       const int dv = g_attn_d40_variant.load(std::memory_order_relaxed);
       const int a16 = dv >= 0 ? dv : a16_env;
       const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
-      if (a16 == 2 && !a.causal) {          // mixed 32x32 QK^T / 16x16 P.V (round 5)
-        if (blocks8 >= 512) launch_mx<8>(a, s);
-        else launch_mx<4>(a, s);
-      } else if (a16 && !a.causal) {
+      // (variant 2, the mixed 32x32 QK^T / 16x16 P.V kernel, is archived: tools/archive/attn_mx_d40.hip.txt)
+      if (a16 && !a.causal) {
         // 8-wave blocks from 256 of them: the 4-wave build takes 130 registers (3 waves per SIMD),
         // and at batch 1 (B = 2, 256 eight-wave blocks) the 8-wave block is 10 % faster
         // (profiles/r5_attn_d40_nw8_batch1_ab.txt).  CASSMANTLE_ATTN16_NW8_MIN overrides (A/B knob)

@@ -803,6 +803,28 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos0, at::Tensor& q_out, a
 }
 
 // one query token per sequence: q [B, H, d], caches [B, L, Hk, d], lens [B] -> out [B, H, d]
+void lm_sample(const at::Tensor& logits, const at::Tensor& noise, const at::Tensor& eos_bias, int64_t eos,
+               double temperature, int64_t k, at::Tensor& step, at::Tensor& out, at::Tensor& tok, at::Tensor& pos,
+               at::Tensor& lens) {
+  CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_CONTIG(noise); CHECK_CONTIG(out);
+  const int64_t V = logits.size(-1);
+  TORCH_CHECK(logits.numel() == V, "lm_sample: batch-1 logits [1, V]");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "lm_sample: f32 / bf16 logits");
+  TORCH_CHECK(noise.scalar_type() == at::kFloat && noise.numel() % V == 0, "lm_sample: noise [steps, 1, V] f32");
+  TORCH_CHECK(eos_bias.scalar_type() == at::kFloat && eos_bias.numel() == noise.numel() / V,
+              "lm_sample: eos_bias [steps] f32");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == eos_bias.numel(), "lm_sample: out [steps, 1] int64");
+  TORCH_CHECK(step.scalar_type() == at::kLong && tok.scalar_type() == at::kLong && step.numel() == 1 && tok.numel() == 1,
+              "lm_sample: step / token int64 scalars");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && lens.scalar_type() == at::kInt, "lm_sample: pos / lens int32");
+  TORCH_CHECK(k >= 1 && temperature > 0, "lm_sample: k >= 1, temperature > 0");
+  launch_lm_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, (int)V, noise.data_ptr<float>(),
+                   eos_bias.data_ptr<float>(), (int)eos, (float)temperature, (int)k,
+                   reinterpret_cast<long long*>(step.data_ptr<int64_t>()), reinterpret_cast<long long*>(out.data_ptr<int64_t>()),
+                   reinterpret_cast<long long*>(tok.data_ptr<int64_t>()), pos.data_ptr<int>(), lens.data_ptr<int>(),
+                   cur_stream());
+}
+
 void decode_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                       const at::Tensor& lens, at::Tensor& out, double scale) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
@@ -895,6 +917,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("advance_step", &advance_step, nogil());
   m.def("zero_", &zero_, nogil());
   m.def("prefetch", &prefetch, nogil());
+  m.def("lm_sample", &lm_sample, nogil());
   m.def("cu_mask_stream", &cu_mask_stream);
   m.def("cu_count", &cu_count);
   m.def("softmax_rows", &softmax_rows, nogil());

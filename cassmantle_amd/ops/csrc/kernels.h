@@ -166,6 +166,11 @@ struct DecodeArgs {
   float scale;
 };
 int decode_splits(int B, int Hk, int L);
+// decode-step sampler (batch 1): top-k of logits / T (+ EOS bias of the step) + Gumbel-max with
+// the step's noise row, then token / position / length / step counter updated on the device
+void launch_lm_sample(const void* logits, int logits_f32, int V, const float* noise, const float* eos_bias, int eos,
+                      float temperature, int k, long long* step, long long* out, long long* tok, int* pos, int* lens,
+                      hipStream_t s);
 void launch_decode_attention(const DecodeArgs& a, int ns, hipStream_t s);
 
 // scorer

@@ -16,6 +16,11 @@
 // * decode_attn_kernel: one query token per sequence against the cache, GQA (a block serves the
 //   G query heads of one KV head so K/V rows are read once), split over the key axis so a batch-1
 //   decode still fills the chip, exp2-domain online softmax, then decode_combine_kernel.
+// * lm_sample_kernel: the decode step's sampler in ONE launch (was ATen topk + gather + argmax +
+//   index_copy inside the captured graph): logits / T (+ the step's EOS bias), the top-k set by a
+//   4-pass 8-bit radix select on order-preserving float keys (ties at the k-th value resolved to
+//   the lowest vocabulary ids), Gumbel-max over the set with the step's noise row, and the
+//   device-side state update (token, position, cache length, step counter).
 #include "common.h"
 #include "kernels.h"
 
@@ -440,7 +445,135 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_attn_kernel(DecodeArgs a) 
   decode_combine<D>(a, b, hk, G, ns, nact);
 }
 
+// ------------------------------------------------------------------------------------ sampler
+// Contract (ops/reference.py lm_sample): v = logit / T, v[eos] += eos_bias[step]; the k largest v
+// with ties broken by the LOWER id; among them the id maximising v + noise[step][id] (ties: larger
+// v, then lower id); out[step] = tok = id; pos, lens, step += 1.  One block, batch 1.
+constexpr int SAMPLE_THREADS = 1024;
+
+CM_DEVICE unsigned fkey(float f) {                  // order-preserving float -> uint32
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <bool F32>
+__global__ void __launch_bounds__(SAMPLE_THREADS) lm_sample_kernel(const void* __restrict__ logits, int V,
+                                                                   const float* __restrict__ noise,
+                                                                   const float* __restrict__ eos_bias, int eos,
+                                                                   float temp, int k, long long* __restrict__ step_p,
+                                                                   long long* __restrict__ out,
+                                                                   long long* __restrict__ tok,
+                                                                   int* __restrict__ pos, int* __restrict__ lens) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned s_prefix, s_rem, s_eq, s_cut;
+  __shared__ float r_sc[SAMPLE_THREADS / 64], r_v[SAMPLE_THREADS / 64];
+  __shared__ int r_id[SAMPLE_THREADS / 64];
+  const int tid = threadIdx.x;
+  const long long step = *step_p;
+  const float eb = eos_bias[step];
+  auto value = [&](int i) -> float {
+    const float l = F32 ? reinterpret_cast<const float*>(logits)[i] : bf2f(reinterpret_cast<const uint16_t*>(logits)[i]);
+    float v = l / temp;
+    if (i == eos) v += eb;
+    return v;
+  };
+  // ---- radix select of the k-th largest key, 8 bits per pass from the top
+  unsigned prefix = 0, mask = 0, rem = (unsigned)min(k, V);
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += SAMPLE_THREADS) {
+      const unsigned key = fkey(value(i));
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned above = 0;
+      int d = 255;
+      for (; d > 0; --d) {                         // digits from the top until rem is reached
+        if (above + hist[d] >= rem) break;
+        above += hist[d];
+      }
+      s_prefix = prefix | ((unsigned)d << shift);
+      s_rem = rem - above;
+      s_eq = hist[d];                              // after the last pass: keys equal to the k-th
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    rem = s_rem;
+    mask |= 255u << shift;
+  }
+  // ---- ties at the k-th key: keep the `rem` lowest ids (only when more keys equal it)
+  if (tid == 0) s_cut = 0x7fffffff;
+  __syncthreads();
+  if (s_eq > rem) {
+    __shared__ unsigned wcnt[SAMPLE_THREADS / 64];
+    unsigned need = rem;
+    for (int base = 0; base < V && need > 0; base += SAMPLE_THREADS) {
+      const int i = base + tid;
+      const bool eq = i < V && fkey(value(i)) == prefix;
+      const unsigned long long bal = __ballot(eq);
+      const int lane = tid & 63, w = tid >> 6;
+      if (lane == 0) wcnt[w] = (unsigned)__popcll(bal);
+      __syncthreads();
+      unsigned before = 0, total = 0;
+      for (int j = 0; j < SAMPLE_THREADS / 64; ++j) {
+        if (j < w) before += wcnt[j];
+        total += wcnt[j];
+      }
+      const unsigned rank = before + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+      if (eq && rank == need - 1) s_cut = (unsigned)i;   // the last tied id that is kept
+      __syncthreads();
+      if (total >= need) break;
+      need -= total;
+    }
+    __syncthreads();
+  }
+  const unsigned cut = s_cut;
+  // ---- Gumbel-max over the top-k set
+  float best = -INFINITY, bv = -INFINITY;
+  int bid = 0x7fffffff;
+  const float* g = noise + step * (long long)V;
+  for (int i = tid; i < V; i += SAMPLE_THREADS) {
+    const float v = value(i);
+    const unsigned key = fkey(v);
+    if (key > prefix || (key == prefix && (unsigned)i <= cut)) {
+      const float sc = v + g[i];
+      if (sc > best || (sc == best && (v > bv || (v == bv && i < bid)))) { best = sc; bv = v; bid = i; }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64), ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bid, o, 64);
+    if (ob > best || (ob == best && (ov > bv || (ov == bv && oi < bid)))) { best = ob; bv = ov; bid = oi; }
+  }
+  if ((tid & 63) == 0) { r_sc[tid >> 6] = best; r_v[tid >> 6] = bv; r_id[tid >> 6] = bid; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 1; j < SAMPLE_THREADS / 64; ++j)
+      if (r_sc[j] > best || (r_sc[j] == best && (r_v[j] > bv || (r_v[j] == bv && r_id[j] < bid)))) {
+        best = r_sc[j]; bv = r_v[j]; bid = r_id[j];
+      }
+    out[step] = bid;
+    tok[0] = bid;
+    pos[0] += 1;
+    lens[0] += 1;
+    *step_p = step + 1;
+  }
+}
+
 }  // namespace
+
+void launch_lm_sample(const void* logits, int logits_f32, int V, const float* noise, const float* eos_bias, int eos,
+                      float temperature, int k, long long* step, long long* out, long long* tok, int* pos, int* lens,
+                      hipStream_t s) {
+  if (logits_f32)
+    hipLaunchKernelGGL(lm_sample_kernel<true>, dim3(1), dim3(SAMPLE_THREADS), 0, s, logits, V, noise, eos_bias, eos,
+                       temperature, k, step, out, tok, pos, lens);
+  else
+    hipLaunchKernelGGL(lm_sample_kernel<false>, dim3(1), dim3(SAMPLE_THREADS), 0, s, logits, V, noise, eos_bias, eos,
+                       temperature, k, step, out, tok, pos, lens);
+}
 
 bool launch_gemv(const GemmArgs& p, hipStream_t s) {
   const long long ldw = p.ldw ? p.ldw : p.K;

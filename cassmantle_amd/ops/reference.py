@@ -245,3 +245,24 @@ def mean_pool_l2(hidden, lens):
     m = (torch.arange(T, device=hidden.device)[None, :] < lens.to(hidden.device)[:, None]).float()
     s = (hidden.float() * m[..., None]).sum(1) / m.sum(1, keepdim=True).clamp_min(1.0)
     return s / s.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+
+
+def lm_sample(logits, noise, eos_bias, eos: int, temperature: float, k: int, step, out, tok, pos, lens) -> None:
+    """Decode-step sampler (the contract of lm.hip's lm_sample_kernel), graph-capturable: v =
+    logits / T with the step's EOS bias added at ``eos``; the k largest v (stable: ties keep the
+    LOWER id); the id maximising v + noise[step] among them (first in that order on ties); then
+    out[step] = tok = id and pos, lens, step advance by one."""
+    lg = logits.float().reshape(1, -1) / temperature
+    V = lg.shape[-1]
+    if 0 <= eos < V:
+        lg[:, eos] += eos_bias.index_select(0, step)
+    srt = torch.sort(lg, dim=-1, descending=True, stable=True)
+    vals, ids = srt.values[:, :k], srt.indices[:, :k]
+    g = noise.index_select(0, step)[0].gather(1, ids)
+    choice = (vals + g).argmax(dim=-1, keepdim=True)
+    nxt = ids.gather(1, choice)[:, 0]
+    out.index_copy_(0, step, nxt[None])
+    tok.copy_(nxt)
+    pos.add_(1)
+    lens.add_(1)
+    step.add_(1)

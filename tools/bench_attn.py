@@ -63,12 +63,6 @@ def main():
                 ops.attention(q, k, v)
                 ops.set_attention_d40_variant(None)
             arms["bf16_32x32"] = old_kernel
-
-            def mixed_kernel():
-                ops.set_attention_d40_variant("mixed")
-                ops.attention(q, k, v)
-                ops.set_attention_d40_variant(None)
-            arms["bf16_mixed"] = mixed_kernel
         if d == 64:
             arms["fp8"] = lambda: ops.attention(q, k, v, fp8="force")
             kv8 = ops.pack_kv_fp8(k, v)          # cross-attention: packed once per text context
@@ -83,7 +77,6 @@ def main():
                 "bf16_vs_sdpa": round(med["sdpa"] / med["bf16"], 3)}
         if "bf16_32x32" in med:
             line["d40_16x16_vs_32x32"] = round(med["bf16_32x32"] / med["bf16"], 3)
-            line["d40_16x16_vs_mixed"] = round(med["bf16_mixed"] / med["bf16"], 3)
         if "fp8" in med:
             line["fp8_vs_bf16"] = round(med["bf16"] / med["fp8"], 3)
             line["fp8_prepacked_vs_bf16"] = round(med["bf16"] / med["fp8_prepacked"], 3)

@@ -8,6 +8,9 @@ mkdir -p $O
 CASSMANTLE_EXT_SO=variants/gemm_pf2.so timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 \
   --timeout-method thread -m gpu -k "gemm or conv" -p no:cacheprovider > $O/tests_pf2.txt 2>&1 || { tail -30 $O/tests_pf2.txt; exit 1; }
 tail -1 $O/tests_pf2.txt
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_lm.py tests/test_parallel_gpu.py -x -q --timeout 200 \
+  --timeout-method thread -m gpu -k "lm_sample or d40 or lm_gpu or supervised" -p no:cacheprovider > $O/tests_new.txt 2>&1 || { tail -40 $O/tests_new.txt; exit 1; }
+tail -1 $O/tests_new.txt
 for rep in 1 2; do
   for v in tree pf1 pf2; do
     so=""; [ $v != tree ] && so=variants/gemm_$v.so
