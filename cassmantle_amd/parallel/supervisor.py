@@ -924,7 +924,10 @@ class GroupSupervisor:
         n = int(np.prod(shape))
         src = self._inbox[key][:n].view(shape)
         dev = torch.device(self.frontend_device) if self.frontend_device else None
-        if dev is None or dev.type != "cuda":
+        diag = os.environ.get("CASSMANTLE_IPC_DIAG", "")     # round-6 diagnosis of the live A/B
+        if diag == "noland":
+            return [np.zeros(shape[1:], np.uint8) for _ in range(shape[0])]
+        if dev is None or dev.type != "cuda" or diag == "hostland":
             host = src.cpu().numpy()
             return [host[i].copy() for i in range(shape[0])]
         if self._land_stream is None:
@@ -932,7 +935,14 @@ class GroupSupervisor:
         t0 = time.perf_counter()
         dst = torch.empty(shape, dtype=torch.uint8, device=dev)
         with torch.cuda.stream(self._land_stream):
-            dst.copy_(src, non_blocking=True)
+            if src.device == dev and os.environ.get("CASSMANTLE_IPC_COPY", "kernel") == "kernel":
+                # the in-tree 16-byte copy kernel: the runtime's D2D copy of IPC-imported memory
+                # (torch copy_ -> hipMemcpyAsync) cost the co-located worker 14 % of its images/s
+                # on one GPU (profiles/r6_live_ipc_diag.txt)
+                from .. import ops
+                ops.copy_(dst, src)
+            else:
+                dst.copy_(src, non_blocking=True)
         self._land_stream.synchronize()      # the worker may overwrite its outbox from its next round
         self.land_us.append((time.perf_counter() - t0) * 1e6)
         return [DeviceImage(dst[i]) for i in range(shape[0])]

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6: ipc landing through the in-tree copy kernel (default now) vs torch copy_ vs pipe, same box x2
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r6h
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_parallel_gpu.py -x -q --timeout 200 --timeout-method thread -m gpu -k ipc -p no:cacheprovider > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+tail -1 $O/tests.txt
+for rep in 1 2; do
+  for v in kernel torchcopy pipe; do
+    t=ipc; [ $v = pipe ] && t=pipe
+    c=kernel; [ $v = torchcopy ] && c=torch
+    CASSMANTLE_IPC_COPY=$c timeout -k 10 300 python tools/bench_live.py --gpus 1 --transport $t --seconds 15 --idle-s 3 > $O/live_${v}_$rep.json 2> $O/live_${v}_$rep.err || { tail -20 $O/live_${v}_$rep.err; exit 1; }
+    echo "live v=$v rep=$rep $(python -c "import json;d=json.loads(open('$O/live_${v}_$rep.json').read().strip().splitlines()[-1]);print(d['images_per_s'], d['load_p50_ms'], d['load_p99_ms'], d.get('transport'), d.get('land_us_p50'), d['rounds'])")"
+  done
+done
