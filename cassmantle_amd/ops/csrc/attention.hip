@@ -768,6 +768,12 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
 #ifndef F8_VEARLY
 #define F8_VEARLY 1
 #endif
+// F8_PIPE (two-stage blocks): the P.V MFMAs of tile t are issued in the NEXT step, right after
+// tile t+1's S MFMAs, so they fill the S latency and tile t+1's softmax runs while they retire
+// (P and the V fragments of tile t are carried across the step's barrier in registers)
+#ifndef F8_PIPE
+#define F8_PIPE 1
+#endif
 constexpr int F8_KSTR = 80;   // LDS row stride (bytes) of the 64-byte fp8 rows: 16-lane groups
                               // of ds_read_b128 hit disjoint banks (20 r mod 64 distinct)
 
@@ -928,6 +934,16 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
   for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
   const i32x8_t ones8 = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
                          0x38383838, 0x38383838, 0x38383838, 0x38383838};   // e4m3 1.0
+  constexpr bool PIPE = F8_PIPE && DB && F8_VEARLY;
+  i32x8_t pf_prev, vf_prev[2];             // PIPE: the previous tile's P and V fragments
+  bool pend = false;
+  auto pv_mfmas = [&](const i32x8_t& p8, const i32x8_t* v8) {
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc)
+      oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v8[dc], p8, oacc[dc], 0, 0, 0, 127, 0, 127);
+    if constexpr (ONES)
+      lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, p8, lsum, 0, 0, 0, 127, 0, 127);
+  };
   for (int st = 0; st < nsteps; ++st) {
     const bool more = st + 1 < nsteps;
     if (more) { F8_GLOAD(st + 1) }
@@ -935,6 +951,10 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
     const uint8_t* const Kw = lds + cur + ks * TILE_B;
     const uint8_t* const Vw = lds + cur + NS * TILE_B + ks * TILE_B;
     const int t = st * NS + ks;
+    if (PIPE && !(t < ntiles) && pend) {   // this split's last tile was the previous one
+      pv_mfmas(pf_prev, vf_prev);
+      pend = false;
+    }
     if (t < ntiles) {                      // wave-uniform: the last step may not reach every split
       f32x16_t sacc[2];
 #pragma unroll
@@ -957,6 +977,10 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
           const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
           vfe[dc] = i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
         }
+      }
+      if constexpr (PIPE) {                // the previous tile's P.V behind this tile's S MFMAs
+        if (pend) pv_mfmas(pf_prev, vf_prev);
+        pend = false;
       }
       const int kbase = t * KT;
       const bool need_mask = (kbase + KT > nk) || (a.causal && kbase + KT - 1 > q0);
@@ -1035,21 +1059,28 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           pf[4 * hf + c] = (int)f8x4(sacc[hf][4 * c], sacc[hf][4 * c + 1], sacc[hf][4 * c + 2], sacc[hf][4 * c + 3]);
+      if constexpr (PIPE) {
+        pf_prev = pf;
+        vf_prev[0] = vfe[0];
+        vf_prev[1] = vfe[1];
+        pend = true;
+      } else {
 #pragma unroll
-      for (int dc = 0; dc < 2; ++dc) {
-        i32x8_t vf;
-        if constexpr (F8_VEARLY) {
-          vf = vfe[dc];
-        } else {
-          const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
-          const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
-          const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
-          vf = i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+        for (int dc = 0; dc < 2; ++dc) {
+          i32x8_t vf;
+          if constexpr (F8_VEARLY) {
+            vf = vfe[dc];
+          } else {
+            const uint8_t* vp = Vw + (dc * 32 + ql) * F8_KSTR + 32 * hlf;
+            const uint4 v0 = *reinterpret_cast<const uint4*>(vp);
+            const uint4 v1 = *reinterpret_cast<const uint4*>(vp + 16);
+            vf = i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+          }
+          oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
         }
-        oacc[dc] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dc], 0, 0, 0, 127, 0, 127);
+        if constexpr (ONES)
+          lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pf, lsum, 0, 0, 0, 127, 0, 127);
       }
-      if constexpr (ONES)
-        lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pf, lsum, 0, 0, 0, 127, 0, 127);
     }
     if constexpr (DB) {
       if (more) {
@@ -1066,6 +1097,7 @@ attn_fp8_kernel(AttnArgs a, int Hk, int Nkp, const uint8_t* __restrict__ K8, con
       }
     }
   }
+  if (PIPE && pend) pv_mfmas(pf_prev, vf_prev);   // the last tile's P.V
   if constexpr (ONES) l_run = lsum[0];
   if constexpr (NS > 1) {
     // merge the key splits: every wave is past the loop's last barrier, so the staging LDS is

@@ -41,15 +41,15 @@ Two dispatch modes:
   job list from the leader, local generation, C2 device-resident RCCL gather to the leader, C4
   barrier (the headline ``bench.py`` runs the same collectives).
 
-Data plane of the async mode (``transport``): ``ipc`` keeps a worker's images in HBM end to end.
+Data plane of the async mode (``transport``): ``ipc`` leaves a worker's images in its HBM.
 The worker copies each round's uint8 images into an outbox buffer in its own HBM, shared with
 the front-end ONCE (a HIP IPC handle, torch's CUDA-tensor reduction over the pipe; re-shared only
-when it grows), and the pipe carries just the round id and shape.  The front-end lands the images
-on its own GPU with one device-to-device copy -- over xGMI when the worker sits on another GPU --
-and hands ``DeviceImage`` handles to the game layer, whose blur cache reads them in place (the
-JPEG of the content needs one host copy).  The worker reuses its outbox only for its next round,
-which is dispatched after the front-end's copy completed.  ``pipe`` sends host arrays instead
-(a CPU front-end, or ``GameConfig.supervisor_transport = "pipe"``).  On the CPU (tests) the
+when it grows), and the pipe carries just the round id and shape.  The front-end lands the round
+with ONE copy of the mapped outbox: by DMA into pinned host memory (``land="host"``, default: the
+JPEG encode needs host pixels) or onto its own GPU (``land="device"``: over xGMI when the worker
+sits on another GPU; ``DeviceImage`` handles whose pixels the blur cache reads in HBM).  The
+worker reuses its outbox only for its next round, which is dispatched after the front-end's copy
+completed.  ``pipe`` pickles host arrays through the pipe instead.  On the CPU (tests) the
 outbox is a shared-memory tensor: the same protocol.
 
 The legacy ``torchrun`` layout (front-end inside rank 0, ``serve.py`` under torchrun) is still
@@ -341,11 +341,14 @@ class GroupSupervisor:
                  worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None,
                  reprobe_s: float = 120.0, dispatch: str = "async",
                  weights: Optional[Dict[str, float]] = None, transport: str = "pipe",
-                 frontend_device: Optional[str] = None) -> None:
+                 frontend_device: Optional[str] = None, land: str = "host") -> None:
         if dispatch not in ("async", "lockstep"):
             raise ValueError(f"dispatch must be async or lockstep, not {dispatch!r}")
         if transport not in ("ipc", "pipe"):
             raise ValueError(f"transport must be ipc or pipe, not {transport!r}")
+        if land not in ("host", "device"):
+            raise ValueError(f"land must be host or device, not {land!r}")
+        self.land = land
         # ``ipc``: images land on ``frontend_device`` (the front-end's GPU; None / cpu: host arrays)
         self.transport = transport
         self.frontend_device = frontend_device
@@ -910,10 +913,15 @@ class GroupSupervisor:
                     fut.set_exception(ImageGenerationError("supervisor closed"))
 
     def _land(self, g: "_Group", w: int, payload: Dict[str, Any]) -> List[Any]:
-        """``ipc`` transport, front-end side: the worker's round is in its outbox (mapped here
-        once per outbox allocation); one device-to-device copy lands it on ``frontend_device``
-        (xGMI when the worker's GPU differs) -> ``DeviceImage`` per image; host arrays without a
-        front-end GPU."""
+        """``ipc`` transport, front-end side: the worker's round is in its HBM outbox (mapped here
+        once per outbox allocation, HIP IPC).  ``land="host"`` (default): one DMA copy of the
+        outbox into pinned host memory -> uint8 arrays (what the JPEG encode needs; no pickling
+        through the pipe).  ``land="device"``: a device-to-device copy onto ``frontend_device``
+        (xGMI when the worker's GPU differs) -> ``DeviceImage`` handles the blur cache reads in
+        HBM.  Measured on one GPU (profiles/r6_live_ipc_diag.txt, r6_live_ipc_land_ab.txt): any
+        front-end KERNEL reading the IPC-imported outbox (runtime blit or the in-tree copy) cost
+        the co-located worker 14 % of its images/s and +1.2 ms score p50, while the DMA landing
+        to the host costs nothing -- hence the default."""
         import torch
         from ..game.content import DeviceImage
         key = (g.epoch, w)
@@ -927,25 +935,33 @@ class GroupSupervisor:
         diag = os.environ.get("CASSMANTLE_IPC_DIAG", "")     # round-6 diagnosis of the live A/B
         if diag == "noland":
             return [np.zeros(shape[1:], np.uint8) for _ in range(shape[0])]
-        if dev is None or dev.type != "cuda" or diag == "hostland":
-            host = src.cpu().numpy()
-            return [host[i].copy() for i in range(shape[0])]
-        if self._land_stream is None:
-            self._land_stream = torch.cuda.Stream(device=dev)
         t0 = time.perf_counter()
-        dst = torch.empty(shape, dtype=torch.uint8, device=dev)
-        with torch.cuda.stream(self._land_stream):
-            if src.device == dev and os.environ.get("CASSMANTLE_IPC_COPY", "kernel") == "kernel":
-                # the in-tree 16-byte copy kernel: the runtime's D2D copy of IPC-imported memory
-                # (torch copy_ -> hipMemcpyAsync) cost the co-located worker 14 % of its images/s
-                # on one GPU (profiles/r6_live_ipc_diag.txt)
-                from .. import ops
-                ops.copy_(dst, src)
-            else:
-                dst.copy_(src, non_blocking=True)
-        self._land_stream.synchronize()      # the worker may overwrite its outbox from its next round
+        if src.device.type != "cuda":                          # CPU workers: shared memory
+            host = src.numpy()
+            out = [host[i].copy() for i in range(shape[0])]
+        elif self.land == "host" or dev is None or dev.type != "cuda":
+            if self._land_stream is None:
+                self._land_stream = torch.cuda.Stream(device=src.device)
+            host = torch.empty(shape, dtype=torch.uint8, pin_memory=True)
+            with torch.cuda.stream(self._land_stream):
+                host.copy_(src, non_blocking=True)
+            self._land_stream.synchronize()    # the worker may overwrite its outbox from its next round
+            h = host.numpy()
+            out = [h[i].copy() for i in range(shape[0])]
+        else:
+            if self._land_stream is None:
+                self._land_stream = torch.cuda.Stream(device=dev)
+            dst = torch.empty(shape, dtype=torch.uint8, device=dev)
+            with torch.cuda.stream(self._land_stream):
+                if src.device == dev and os.environ.get("CASSMANTLE_IPC_COPY", "kernel") == "kernel":
+                    from .. import ops
+                    ops.copy_(dst, src)            # in-tree 16-byte copy kernel (same device)
+                else:
+                    dst.copy_(src, non_blocking=True)
+            self._land_stream.synchronize()
+            out = [DeviceImage(dst[i]) for i in range(shape[0])]
         self.land_us.append((time.perf_counter() - t0) * 1e6)
-        return [DeviceImage(dst[i]) for i in range(shape[0])]
+        return out
 
     def _loop(self) -> None:
         try:

@@ -140,7 +140,8 @@ def _serve_supervised(cfg, args) -> int:
                           stale_s=cfg.game.rank_stale_s, heartbeat_s=cfg.game.rank_heartbeat_s,
                           reprobe_s=cfg.game.device_reprobe_s, dispatch=cfg.game.supervisor_dispatch,
                           weights={devices[0]: cfg.game.frontend_device_weight},
-                          transport=cfg.game.supervisor_transport, frontend_device=devices[0])
+                          transport=cfg.game.supervisor_transport, frontend_device=devices[0],
+                          land=cfg.game.supervisor_land)
     sup.wait_ready()
     if cfg.model.scorer_stream_priority is None:
         cfg.model.scorer_stream_priority = 0      # no generation in this process (config.py)

@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--transport", choices=("ipc", "pipe"), default="ipc",
                     help="supervised async data plane: images land on GPU 0 from the workers' HBM "
                          "outboxes (ipc) or travel as host arrays through the pipes (pipe)")
+    ap.add_argument("--land", choices=("host", "device"), default="host",
+                    help="ipc transport: land each round in pinned host memory (DMA) or on GPU 0")
     ap.add_argument("--weight0", type=float, default=None,
                     help="room share of GPU 0 (the scorer's device); default config.frontend_device_weight")
     ap.add_argument("--slots-per-gpu", type=int, default=1,
@@ -115,7 +117,7 @@ def main_supervised(a) -> None:
     w0 = cfg.game.frontend_device_weight if a.weight0 is None else a.weight0
     sup = GroupSupervisor(cfg, devices, rooms, window_s=0.05, start_timeout_s=1200, dispatch=a.dispatch,
                           weights={devices[0]: w0}, transport=a.transport,
-                          frontend_device="cuda:0" if gpu else None)
+                          frontend_device="cuda:0" if gpu else None, land=a.land)
     if not sup.wait_ready(1500) or not sup.live_devices():
         raise SystemExit(f"worker group did not start: {sup.status()}")
     print(f"[live] worker group up on {sup.live_devices()} in {time.perf_counter() - t_start:.1f} s",
