@@ -770,9 +770,11 @@ void launch_nw(const AttnArgs& a, hipStream_t s) {
 #endif
 // F8_PIPE (two-stage blocks): the P.V MFMAs of tile t are issued in the NEXT step, right after
 // tile t+1's S MFMAs, so they fill the S latency and tile t+1's softmax runs while they retire
-// (P and the V fragments of tile t are carried across the step's barrier in registers)
+// (P and the V fragments of tile t are carried across the step's barrier in registers).
+// Measured 4 % SLOWER on the SDXL self-attention (80.3 -> 83.8 us at 4096 keys, same box,
+// profiles/r6_fp8_pipe_negative.txt): off; kept selectable for A/B builds
 #ifndef F8_PIPE
-#define F8_PIPE 1
+#define F8_PIPE 0
 #endif
 constexpr int F8_KSTR = 80;   // LDS row stride (bytes) of the 64-byte fp8 rows: 16-lane groups
                               // of ds_read_b128 hit disjoint banks (20 r mod 64 distinct)

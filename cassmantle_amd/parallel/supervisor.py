@@ -912,6 +912,18 @@ class GroupSupervisor:
                 if not fut.done():
                     fut.set_exception(ImageGenerationError("supervisor closed"))
 
+    def _stream_for(self, device):
+        """The stream the landing copy runs on.  By default the thread's CURRENT stream (no new
+        stream in the front-end: one more stream was measured to cost the co-located worker 14 %
+        of its images/s -- the GPU's queue scheduler then time-slices more hardware queues,
+        profiles/r6_live_ipc_stream_ab.txt); CASSMANTLE_IPC_STREAM=own: a dedicated stream."""
+        import torch
+        if os.environ.get("CASSMANTLE_IPC_STREAM", "current") == "own":
+            if self._land_stream is None:
+                self._land_stream = torch.cuda.Stream(device=device)
+            return self._land_stream
+        return torch.cuda.current_stream(device)
+
     def _land(self, g: "_Group", w: int, payload: Dict[str, Any]) -> List[Any]:
         """``ipc`` transport, front-end side: the worker's round is in its HBM outbox (mapped here
         once per outbox allocation, HIP IPC).  ``land="host"`` (default): one DMA copy of the
@@ -940,25 +952,23 @@ class GroupSupervisor:
             host = src.numpy()
             out = [host[i].copy() for i in range(shape[0])]
         elif self.land == "host" or dev is None or dev.type != "cuda":
-            if self._land_stream is None:
-                self._land_stream = torch.cuda.Stream(device=src.device)
+            stream = self._stream_for(src.device)
             host = torch.empty(shape, dtype=torch.uint8, pin_memory=True)
-            with torch.cuda.stream(self._land_stream):
+            with torch.cuda.stream(stream):
                 host.copy_(src, non_blocking=True)
-            self._land_stream.synchronize()    # the worker may overwrite its outbox from its next round
+            stream.synchronize()               # the worker may overwrite its outbox from its next round
             h = host.numpy()
             out = [h[i].copy() for i in range(shape[0])]
         else:
-            if self._land_stream is None:
-                self._land_stream = torch.cuda.Stream(device=dev)
+            stream = self._stream_for(dev)
             dst = torch.empty(shape, dtype=torch.uint8, device=dev)
-            with torch.cuda.stream(self._land_stream):
+            with torch.cuda.stream(stream):
                 if src.device == dev and os.environ.get("CASSMANTLE_IPC_COPY", "kernel") == "kernel":
                     from .. import ops
                     ops.copy_(dst, src)            # in-tree 16-byte copy kernel (same device)
                 else:
                     dst.copy_(src, non_blocking=True)
-            self._land_stream.synchronize()
+            stream.synchronize()
             out = [DeviceImage(dst[i]) for i in range(shape[0])]
         self.land_us.append((time.perf_counter() - t0) * 1e6)
         return out
