@@ -92,9 +92,9 @@ class GameConfig:
     # the front-end lands them on ITS GPU with one device-to-device copy (xGMI between GPUs), where
     # the blur cache reads them; "pipe": host uint8 arrays pickled through the worker's pipe
     supervisor_transport: str = "ipc"
-    # ipc landing on the front-end: "host" (DMA of the worker's HBM outbox into pinned memory) or
-    # "device" (copy onto the front-end GPU; measured 14 % slower on a shared GPU, parallel/supervisor.py)
-    supervisor_land: str = "host"
+    # ipc landing on the front-end: "device" (copy of the worker's HBM outbox onto the front-end
+    # GPU, where the blur cache reads it) or "host" (DMA into pinned memory); both at pipe speed
+    supervisor_land: str = "device"
     # share of the rooms owned by the GPU the front-end's guess scorer also runs on (GPU 0);
     # the other GPUs have weight 1 (parallel.rooms.RoomSharding)
     frontend_device_weight: float = 0.85

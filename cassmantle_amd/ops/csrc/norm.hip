@@ -350,7 +350,14 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_cs_kernel(const uint16_t*
       const float o = fmaf(f[i], sc[j][i], sf[j][i]);
       f[i] = silu ? silu_f(o) : o;
     }
+#if GN_NT_STORE
+    // (A/B knob) streaming store: no write-allocate in L2 / MALL for outputs larger than them
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_nt;
+    const uint4 pk = pack8(f);
+    __builtin_nontemporal_store(u32x4_nt{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_nt*>(yb + rr * C + (tv + T * j) * 8));
+#else
     *reinterpret_cast<uint4*>(yb + rr * C + (tv + T * j) * 8) = pack8(f);
+#endif
   };
   // ---- 3. software-pipelined row loop: group i + 1 is in flight while group i is stored
   for (; r < rend; r += U * R) {
@@ -558,6 +565,9 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
 // per thread or 2048 blocks were slower on the small levels.
 #ifndef GN_APPLY_GEOM
 #define GN_APPLY_GEOM 1
+#endif
+#ifndef GN_NT_STORE
+#define GN_NT_STORE 0
 #endif
 #ifndef GN_APPLY_U
 #define GN_APPLY_U 4

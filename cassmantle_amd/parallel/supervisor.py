@@ -45,9 +45,10 @@ Data plane of the async mode (``transport``): ``ipc`` leaves a worker's images i
 The worker copies each round's uint8 images into an outbox buffer in its own HBM, shared with
 the front-end ONCE (a HIP IPC handle, torch's CUDA-tensor reduction over the pipe; re-shared only
 when it grows), and the pipe carries just the round id and shape.  The front-end lands the round
-with ONE copy of the mapped outbox: by DMA into pinned host memory (``land="host"``, default: the
-JPEG encode needs host pixels) or onto its own GPU (``land="device"``: over xGMI when the worker
-sits on another GPU; ``DeviceImage`` handles whose pixels the blur cache reads in HBM).  The
+with ONE copy of the mapped outbox: by DMA into pinned host memory (the JPEG encode needs host
+pixels, ``land="host"``) or onto its own GPU (``land="device"``, default:
+over xGMI when the worker sits on another GPU; ``DeviceImage`` handles whose pixels the blur
+cache reads in HBM).  The
 worker reuses its outbox only for its next round, which is dispatched after the front-end's copy
 completed.  ``pipe`` pickles host arrays through the pipe instead.  On the CPU (tests) the
 outbox is a shared-memory tensor: the same protocol.
@@ -115,7 +116,9 @@ class DeviceOutbox:
         import torch
         self.device = torch.device(device)
         self.buf = None
-        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # the worker thread's CURRENT stream, not a new one: every extra stream of a process that
+        # shares its GPU was measured to cost the co-located work 14 % (profiles/r6_live_ipc_stream_ab.txt)
+        self.stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
 
     def put(self, images):
         import torch
@@ -341,7 +344,7 @@ class GroupSupervisor:
                  worker_env: Optional[Dict[str, str]] = None, resolution: Optional[int] = None,
                  reprobe_s: float = 120.0, dispatch: str = "async",
                  weights: Optional[Dict[str, float]] = None, transport: str = "pipe",
-                 frontend_device: Optional[str] = None, land: str = "host") -> None:
+                 frontend_device: Optional[str] = None, land: str = "device") -> None:
         if dispatch not in ("async", "lockstep"):
             raise ValueError(f"dispatch must be async or lockstep, not {dispatch!r}")
         if transport not in ("ipc", "pipe"):
@@ -926,14 +929,12 @@ class GroupSupervisor:
 
     def _land(self, g: "_Group", w: int, payload: Dict[str, Any]) -> List[Any]:
         """``ipc`` transport, front-end side: the worker's round is in its HBM outbox (mapped here
-        once per outbox allocation, HIP IPC).  ``land="host"`` (default): one DMA copy of the
-        outbox into pinned host memory -> uint8 arrays (what the JPEG encode needs; no pickling
-        through the pipe).  ``land="device"``: a device-to-device copy onto ``frontend_device``
-        (xGMI when the worker's GPU differs) -> ``DeviceImage`` handles the blur cache reads in
-        HBM.  Measured on one GPU (profiles/r6_live_ipc_diag.txt, r6_live_ipc_land_ab.txt): any
-        front-end KERNEL reading the IPC-imported outbox (runtime blit or the in-tree copy) cost
-        the co-located worker 14 % of its images/s and +1.2 ms score p50, while the DMA landing
-        to the host costs nothing -- hence the default."""
+        once per outbox allocation, HIP IPC).  ``land="device"`` (default): one device-to-device
+        copy onto ``frontend_device`` (xGMI when the worker's GPU differs) -> ``DeviceImage``
+        handles the blur cache reads in HBM.  ``land="host"``: one DMA copy of the outbox into
+        pinned host memory -> uint8 arrays.  Either copy runs on the thread's current stream: a
+        landing stream of its own cost the co-located worker 14 % of its images/s and +1.2 ms
+        score p50, both landings without it run at pipe speed (profiles/r6_live_ipc_stream_ab.txt)."""
         import torch
         from ..game.content import DeviceImage
         key = (g.epoch, w)

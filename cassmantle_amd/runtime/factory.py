@@ -8,6 +8,9 @@
 """
 from __future__ import annotations
 
+import contextlib
+import os
+
 from typing import Callable, Optional
 
 import numpy as np
@@ -81,10 +84,13 @@ def build_blur_fn(cfg: Config, device: Optional[str] = None):
     if not cfg.model.gpu_blur or not dev.startswith("cuda"):
         return None
     from .. import ops
-    stream = torch.cuda.Stream(device=dev)
+    # the blur runs on the calling thread's current stream: a stream of its own in a process that
+    # shares its GPU with a generation worker cost that worker 14 % of its images/s
+    # (profiles/r6_live_ipc_stream_ab.txt); CASSMANTLE_BLUR_STREAM=own restores one
+    stream = torch.cuda.Stream(device=dev) if os.environ.get("CASSMANTLE_BLUR_STREAM") == "own" else None
 
     def blur(img, radius: float):
-        with torch.cuda.stream(stream):
+        with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
             t = getattr(img, "tensor", None)        # DeviceImage: already in this GPU's HBM
             if t is not None and t.device.type == "cuda":
                 x = t.to(dev, non_blocking=False)

@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--transport", choices=("ipc", "pipe"), default="ipc",
                     help="supervised async data plane: images land on GPU 0 from the workers' HBM "
                          "outboxes (ipc) or travel as host arrays through the pipes (pipe)")
-    ap.add_argument("--land", choices=("host", "device"), default="host",
+    ap.add_argument("--land", choices=("host", "device"), default="device",
                     help="ipc transport: land each round in pinned host memory (DMA) or on GPU 0")
     ap.add_argument("--weight0", type=float, default=None,
                     help="room share of GPU 0 (the scorer's device); default config.frontend_device_weight")

@@ -26,6 +26,9 @@ CONV_SHAPES = [(8, 16, 16, 1280, 1280), (8, 16, 16, 2560, 1280), (8, 8, 8, 1280,
 # SDXL (batch 1 x CFG) GroupNorm applies: 128^2 / 64^2 / 32^2 levels incl. the up-block concat widths
 SDXL_GN_SHAPES = [(2, 128, 128, 320), (2, 128, 128, 640), (2, 128, 128, 960), (2, 64, 64, 640),
                   (2, 64, 64, 1280), (2, 64, 64, 1920), (2, 32, 32, 1280), (2, 32, 32, 2560)]
+# SD VAE decoder GroupNorm applies at the bench's batch 4 (512^2 output: 64^2 .. 512^2 levels)
+VAE_GN_SHAPES = [(4, 64, 64, 512), (4, 128, 128, 512), (4, 256, 256, 512), (4, 256, 256, 256),
+                 (4, 512, 512, 256), (4, 512, 512, 128)]
 ITERS = 30
 
 
@@ -98,8 +101,9 @@ if __name__ == "__main__":
     ap.add_argument("--lines", default=None, help="that run's JSON output (for --trace)")
     ap.add_argument("--gn-only", action="store_true", help="only the GroupNorm applies")
     ap.add_argument("--sdxl", action="store_true", help="the SDXL GroupNorm shapes (implies --gn-only)")
+    ap.add_argument("--vae", action="store_true", help="the SD VAE decoder GroupNorm shapes (implies --gn-only)")
     a = ap.parse_args()
     if a.trace:
         from_trace(a.trace, [json.loads(x) for x in open(a.lines) if x.startswith("{")])
     else:
-        run(a.gn_only or a.sdxl, SDXL_GN_SHAPES if a.sdxl else GN_SHAPES)
+        run(a.gn_only or a.sdxl or a.vae, SDXL_GN_SHAPES if a.sdxl else (VAE_GN_SHAPES if a.vae else GN_SHAPES))
