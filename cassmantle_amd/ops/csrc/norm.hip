@@ -566,8 +566,16 @@ void launch_group_norm(const uint16_t* x, const uint16_t* gamma, const uint16_t*
 #ifndef GN_APPLY_GEOM
 #define GN_APPLY_GEOM 1
 #endif
+// Output stores non-temporal (round 6, profiles/r6_gn_apply_variants.txt: 64^2 x 320 at batch 8
+// 12.9 -> 11.3 us, the VAE 256^2 x 512 / 512^2 x 128 applies 114 / 111 -> 87 / 83 us = 6.2-6.5
+// TB/s); GN_U8_RULE: 8 rows per thread in flight for 512..1024-channel tensors of >= 4096 rows
+// per image (64^2 x 640 16.7 vs 18.4 us, the VAE 64^2 x 512 9.2 vs 11.4), 4 elsewhere (the
+// small levels lose with 8)
 #ifndef GN_NT_STORE
-#define GN_NT_STORE 0
+#define GN_NT_STORE 1
+#endif
+#ifndef GN_U8_RULE
+#define GN_U8_RULE 1
 #endif
 #ifndef GN_APPLY_U
 #define GN_APPLY_U 4
@@ -626,6 +634,11 @@ void launch_group_norm_cs(const uint16_t* x, const uint16_t* x2, const long long
   // U rows per thread, at most 16 vector loads (VPT x U) in flight per thread
   constexpr int U = GN_APPLY_U;
   constexpr int U2 = U * 2 > 16 ? 8 : U, U4 = U * 4 > 16 ? 4 : U;
+  if (GN_U8_RULE && C >= 512 && C <= 1024 && S >= 4096) {
+    if (g.VPT == 1) launch_apply<1, 8>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
+    else launch_apply<2, 8>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
+    return;
+  }
   if (g.VPT == 1) launch_apply<1, U>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
   else if (g.VPT == 2) launch_apply<2, U2>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
   else launch_apply<4, U4>(x, x2, stats_a, Ca, stats_b, gamma, beta, y, B, S, C, G, eps, silu, g, s);
