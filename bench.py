@@ -65,7 +65,7 @@ def parse():
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--no-sdxl", action="store_true", help="skip the SDXL fp8 extra (BASELINE config 4)")
     p.add_argument("--no-live", action="store_true", help="skip the in-process live-round extra (config 5)")
-    p.add_argument("--live-seconds", type=float, default=8.0)
+    p.add_argument("--live-seconds", type=float, default=12.0)
     p.add_argument("--live-players", type=int, default=64)
     p.add_argument("--comm-timeout-s", type=float, default=180.0,
                    help="bound on the process-group init and on every blocking collective of a rank")
@@ -75,6 +75,20 @@ def parse():
                         "(rank r on GPU r mod visible) over gloo with a host gather; RCCL refuses "
                         "two ranks on one device, so nccl is refused here")
     return p.parse_args()
+
+
+_ENCODERS: dict = {}
+
+
+def shared_encoder(device):
+    """ONE graph-replayed MiniLM backend (and so one high-priority scorer stream) per process for
+    the scorer measurements and the live round: every further stream of a process shares the
+    GPU's hardware queues with the generation stream (supervisor.py, profiles/r6_live_ipc_stream_ab.txt)."""
+    from cassmantle_amd.scoring.encoder import EncoderBackend
+    key = str(device)
+    if key not in _ENCODERS:
+        _ENCODERS[key] = EncoderBackend(device=key, stream_priority=-1)
+    return _ENCODERS[key]
 
 
 def scorer_bench(device) -> dict:
@@ -92,7 +106,7 @@ def scorer_bench(device) -> dict:
     words = [w for w in load_vocab() if w.isalpha()]
     rng = random.Random(0)
     secrets = ["lantern", "tower"]
-    be = EncoderBackend(device=str(device), stream_priority=-1)
+    be = shared_encoder(device)
 
     def run(batch, iters):
         lat = []
@@ -408,7 +422,9 @@ def run_rank(args, wd: "Watchdog") -> int:
     H = spec.resolution
     gather_buf = None
     gather_ms = []
-    comm = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+    # the C2 gather's stream exists only when there is a gather (a 1-GPU run creates no stream
+    # beyond the pipeline's)
+    comm = torch.cuda.Stream(device=device) if device.type == "cuda" and world > 1 else None
     # gloo (the one-GPU multi-rank rehearsal) gathers host tensors; RCCL gathers in HBM
     host_gather = world > 1 and dist.get_backend() == "gloo"
 
@@ -568,7 +584,7 @@ def live_extra(args, sd, device, room_prompts, negative) -> dict:
     from cassmantle_amd.runtime.live import live_round_inprocess
     from cassmantle_amd.scoring.batcher import BatchingScorer
     from cassmantle_amd.scoring.encoder import EncoderBackend
-    scorer = BatchingScorer(EncoderBackend(device=str(device), stream_priority=-1), 0.01, window_ms=1.0)
+    scorer = BatchingScorer(shared_encoder(device), 0.01, window_ms=1.0)
 
     def gen(step: int) -> int:
         imgs = sd.generate(room_prompts(20_000 + step), negative,
