@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 out=gpurun_out/pmc_$name
 mkdir -p $out
-CMD=${CMD:-"python bench.py --steps 1 --warmup 0 --no-score --no-batch1 --no-graphs $*"}
+CMD=${CMD:-"python bench.py --steps 1 --warmup 0 --no-score --no-batch1 --no-live --no-sdxl --no-graphs $*"}
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/trace -o run -- $CMD > $out/trace.log 2>&1 || { tail -5 $out/trace.log; exit 1; }
 i=0
 for cnt in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
