@@ -103,8 +103,10 @@ def test_injected_process_group_init_failure_is_bounded(mode, extra):
     assert rec["comm"]["world_size"] == 2 and rec["comm"]["backend"] == "gloo"
     if mode == "raise":
         assert "injected process-group init failure on rank 1" in rec["comm"]["error"], rec
-    else:                                       # rank 0's init bound fired
-        assert "rank 0" in rec["comm"]["error"] and "comm-init" in rec["error"], rec
+    else:                                       # a rank's init bound fired (both ranks arm it:
+        # the wedged rank 1 and rank 0 waiting on it expire ~together; the first report wins)
+        assert "comm-init" in rec["error"], rec
+        assert any(f"rank {r}: comm-init" in rec["comm"]["error"] for r in (0, 1)), rec
 
 
 def test_bench_live_supervised_topology():
