@@ -451,6 +451,19 @@ constexpr int A16_NCH = 5;           // staged 16-B chunks per key row (d = 40)
 #ifndef A16_KSTR
 #define A16_KSTR 48                  // K row (elements) of the 16x16 kernel (56 measured slower: r5_attn_d40_mixed_ab)
 #endif
+// A16_BUFLD: K/V staging loads through per-tile buffer resources (base = the tile's first key,
+// num_records = the bytes of its valid keys), so keys past nk and idle lanes read zeros from the
+// buffer unit's range check: no zero-fill moves, compares, exec masking or 64-bit address VALU
+// per tile.  A16_UNROLL2: the tile loop unrolled by two, so both LDS buffers' addresses are
+// compile-time immediates.  The kernel is bound by the SIMD's issue slots (v_exp_f32 8 cycles,
+// MFMA 8 of its 16, VALU 4: ~800 issue cycles per wave-tile against 448 of MFMA), so every VALU
+// taken off the tile counts (round 6).
+#ifndef A16_BUFLD
+#define A16_BUFLD 1
+#endif
+#ifndef A16_UNROLL2
+#define A16_UNROLL2 1
+#endif
 
 template <int NW>
 __global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
@@ -534,9 +547,33 @@ __global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
     c_ks[i] = (long long)key * a.k_sn + ch * 8;
     c_vs[i] = (long long)key * a.v_sn + ch * 8;
   }
+  int c_kvo[LD], c_vvo[LD];                 // A16_BUFLD: byte voffsets (idle lanes out of range)
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const bool on = tid + i * THREADS < CH;
+    c_kvo[i] = on ? (int)(c_ks[i] * 2) : (int)0x80000000;
+    c_vvo[i] = on ? (int)(c_vs[i] * 2) : (int)0x80000000;
+  }
   auto gload = [&](int t) {
     const int kbase = t * KT;
     const long long ko = (long long)kbase * a.k_sn, vo = (long long)kbase * a.v_sn;
+    if constexpr (A16_BUFLD) {
+      // wave-uniform resources: all scalar work; the range check covers voffset only
+      const int left = nk - kbase;
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(Kp + ko), (short)0, (int)((long long)left * a.k_sn * 2), 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(Vp + vo), (short)0, (int)((long long)left * a.v_sn * 2), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < LD; ++i) {
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rk, c_kvo[i], 0, 0);
+        const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(rv, c_vvo[i], 0, 0);
+        kr[i] = make_uint4(x.x, x.y, x.z, x.w);
+        vr[i] = make_uint4(y.x, y.y, y.z, y.w);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < LD; ++i) {
       uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
@@ -576,10 +613,9 @@ __global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
   // tr-read geometry: lane 4q'+p of a 16-lane group addresses row q', columns 4p..4p+3
   const int tr_off = (4 * g + (li >> 2)) * A16_STR + 4 * (li & 3);
 
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](const int t, const int bo) {
     const bool more = t + 1 < ntiles;
     if (more) gload(t + 1);
-    const int bo = (t & 1) * BUF;
     const uint16_t* Ks = lds + bo;
     const uint16_t* Vs = lds + bo + KTILE;
 
@@ -682,6 +718,14 @@ __global__ void __launch_bounds__(64 * NW, 2) attn16_d40_kernel(AttnArgs a) {
     // previous barrier
     if (more) lstore(BUF - bo);
     __syncthreads();
+  };
+  if constexpr (A16_UNROLL2) {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, 0);
+      if (t + 1 < ntiles) tile(t + 1, BUF);
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) tile(t, (t & 1) * BUF);
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l, l = O^T row 40 (lanes 32..47, register 0 of block 2)
