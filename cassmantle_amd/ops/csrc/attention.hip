@@ -1282,7 +1282,10 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
       const int a16 = dv >= 0 ? dv : a16_env;
       const long long blocks8 = (long long)((a.Nq + 255) / 256) * a.H * a.B;
       // (variant 2, the mixed 32x32 QK^T / 16x16 P.V kernel, is archived: tools/archive/attn_mx_d40.hip.txt)
-      if (a16 && !a.causal) {
+      // (the 16x16 kernel's per-tile buffer resources address a (batch, head)'s keys with 32-bit
+      // byte counts: spans of 2 GiB or more take the 32x32 kernel)
+      const bool span_ok = (long long)a.Nk * a.k_sn * 2 < (1LL << 31) && (long long)a.Nk * a.v_sn * 2 < (1LL << 31);
+      if (a16 && !a.causal && (span_ok || !A16_BUFLD)) {
         // 8-wave blocks from 256 of them: the 4-wave build takes 130 registers (3 waves per SIMD),
         // and at batch 1 (B = 2, 256 eight-wave blocks) the 8-wave block is 10 % faster
         // (profiles/r5_attn_d40_nw8_batch1_ab.txt).  CASSMANTLE_ATTN16_NW8_MIN overrides (A/B knob)
