@@ -1,6 +1,5 @@
 #!/bin/bash
-# round 6: A-in-registers GEMM epilogue with the activation / residual as chunk-uniform template
-# choices (AREG_EPI_SPLIT, in-tree) vs the previous source (variants/areg_old.so): numerics, bench x2
+# round 6: gated A-in-registers GEMM tiles without residual registers (in-tree) vs the previous source (variants/areg_old.so): numerics, bench x2
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r6r
