@@ -71,13 +71,13 @@ def live_round_inprocess(generate: Callable[[int], int], scorer, players: int = 
     t0 = time.perf_counter()
     th.start()
     load = asyncio.run(run_players(scorer, players, seconds, think_ms, seed + 7))
-    images = done["images"]
+    images, generations = done["images"], done["generations"]   # one snapshot: finished work only
     elapsed = time.perf_counter() - t0
     stop.set()
     th.join()
     if err:
         raise err[0]
-    out = {"images_per_s": round(images / elapsed, 3), "generations": done["generations"],
+    out = {"images_per_s": round(images / elapsed, 3), "generations": generations,
            "load_p50_ms": round(pct(load, 50), 3), "load_p99_ms": round(pct(load, 99), 3),
            "requests": len(load), "seconds": round(elapsed, 2), "players": players}
     if idle:
