@@ -31,10 +31,13 @@ CM_DEVICE uint32_t pack2(float a, float b) {
 }
 
 // four fp32 -> four OCP e4m3 bytes (little-endian)
+// (one asm pair: through the builtin, hipcc zero-fills the destination before the first
+// half-word write -- a v_mov per packed word, 8 per fp8 attention tile, round 6 ISA)
 CM_DEVICE uint32_t f8x4(float a, float b, float c, float d) {
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  return (uint32_t)w;
+  uint32_t w;
+  asm("v_cvt_pk_fp8_f32 %0, %1, %2\n\tv_cvt_pk_fp8_f32 %0, %3, %4 op_sel:[0,0,1]"
+      : "=&v"(w) : "v"(a), "v"(b), "v"(c), "v"(d));
+  return w;
 }
 
 // slot of key offset kk (0..63) inside its 64-key block of the fp8 attention kernel's V8t image
